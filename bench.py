@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Benchmark: QP solves/s for the TRON1 13-state / 6-input / N=10 SRBM MPC (BASELINE.json
+metric), batch 65,536 per GPU, 1..8 MI355X (one process per GPU, weak scaling: config D is
+524,288 = 65,536 x 8).
+
+One step = one pass of the hot path over the whole per-GPU batch, inputs resident in HBM:
+  k_condense (linearise + exp(M Ts) + Ad^k Bd + H, f) -> k_solve (Goldfarb-Idnani QP) ->
+  k_select_min (min-cost key) -> [N>1] RCCL MIN all-reduce of the 8-byte key + broadcast of
+  the winner's U (480 B).
+
+Prints ONE JSON line on rank 0 (driver contract).
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config B|C|L]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mpc-limx-control_amd"))
+
+FP64_PEAK_TFLOPS = 78.6  # MI355X dense FP64 (vector = matrix), AMD spec; SURVEY.md 8d
+
+
+def algorithmic_flops(nx: int, nu: int, N: int):
+    """SURVEY.md section 8d structure-exploiting flop model, split per kernel."""
+    n = nx + nu
+    nV = nu * N
+    F_disc = 8 * n ** 3 + (2.0 / 3.0) * n ** 3
+    F_pow = (N - 1) * 2 * nx ** 3
+    F_phi = (N - 1) * 2 * nx ** 2 * nu
+    F_W = (N * (N + 1) / 2) * 2 * nx ** 2 * nu
+    F_H = sum((i + 1) * (N - i) for i in range(N)) * 2 * nu ** 2 * nx
+    F_f = N * 2 * nx ** 2 + (N * (N + 1) / 2) * 2 * nx * nu
+    F_chol = nV ** 3 / 3.0
+    F_iter = 4 * nV ** 2
+    return dict(condense=F_disc + F_pow + F_phi + F_W + F_H + F_f, solve_fixed=F_chol,
+                per_iter=F_iter)
+
+
+def algorithmic_bytes(nx: int, nu: int, N: int):
+    """read x0, xref, 7 linearisation scalars, contact; write U, cost, status."""
+    nV = nu * N
+    return (nx + nx * (N + 1) + 7 + 2 * N + nV + 1) * 8 + 4
+
+
+def cpu_baseline(p, batch, budget_s=12.0):
+    """The oracle (C restatement of the reference path, OpenMP over the batch) on the host."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # CPU baseline leg only
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    n0 = min(256, batch["x0"].shape[0])
+    sub = {k: v[:n0] for k, v in batch.items()}
+    t = time.perf_counter()
+    oracle.srbm_batch(p, sub["x0"], sub["xref"], sub["lin"], sub["contact"], nthreads=threads)
+    rate0 = n0 / max(1e-6, time.perf_counter() - t)
+    n = int(min(batch["x0"].shape[0], max(n0, rate0 * budget_s)))
+    sub = {k: v[:n] for k, v in batch.items()}
+    t = time.perf_counter()
+    o = oracle.srbm_batch(p, sub["x0"], sub["xref"], sub["lin"], sub["contact"], nthreads=threads)
+    dt = time.perf_counter() - t
+    return dict(value=n / dt, unit="QP/s", cores=threads, kind="port",
+                sample=f"first {n} instances of the rank-0 batch, oracle/mpcqp_oracle.c "
+                       f"(reference-literal dense condensing + Goldfarb-Idnani), OpenMP "
+                       f"{threads} threads, {dt:.1f} s"), o
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=65536, help="instances per GPU")
+    ap.add_argument("--config", default="B")
+    ap.add_argument("--seed", type=int, default=20250404)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import mpcqp
+    from mpcqp.engine import BatchEngine, decode_key
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+
+    p = mpcqp.model_params(args.config)
+    B = args.batch
+    batch = mpcqp.make_batch(p, B, seed=args.seed + rank)
+    eng = BatchEngine(p, device=local)
+    d = eng.upload(batch)
+    nV = eng.nV
+    H = torch.empty((B, nV, nV), dtype=torch.float64, device=f"cuda:{local}")
+    f = torch.empty((B, nV), dtype=torch.float64, device=f"cuda:{local}")
+    ubest = torch.zeros(nV, dtype=torch.float64, device=f"cuda:{local}")
+
+    def step():
+        eng.condense(d, H, f)
+        eng.solve_qp(d, H, f)
+        key = eng.select_min(d, index_base=rank * B)
+        if world > 1:
+            dist.all_reduce(key, op=dist.ReduceOp.MIN)
+            _, gidx = decode_key(int(key.item()))
+            owner = gidx // B
+            if owner == rank:
+                ubest.copy_(d["U"][gidx % B])
+            dist.broadcast(ubest, src=owner)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        e = ev[s]
+        e[0].record(stream)
+        eng.condense(d, H, f)
+        e[1].record(stream)
+        eng.solve_qp(d, H, f)
+        e[2].record(stream)
+        key = eng.select_min(d, index_base=rank * B)
+        e[3].record(stream)
+        if world > 1:
+            dist.all_reduce(key, op=dist.ReduceOp.MIN)
+            _, gidx = decode_key(int(key.item()))
+            owner = gidx // B
+            if owner == rank:
+                ubest.copy_(d["U"][gidx % B])
+            dist.broadcast(ubest, src=owner)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    cond_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    solve_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    status = d["status"].cpu().numpy()
+    iters = d["iters"].cpu().numpy()
+    solved = float(np.mean(status == 0))
+
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        total = B * world
+        fl = algorithmic_flops(p["nx"], p["nu"], p["N"])
+        f_cond = fl["condense"] * B
+        f_solve = (fl["solve_fixed"] + fl["per_iter"] * float(iters.mean())) * B
+        dom = "solve" if solve_ms >= cond_ms else "condense"
+        dom_ms = max(solve_ms, cond_ms)
+        dom_flops = f_solve if dom == "solve" else f_cond
+        achieved = dom_flops / (dom_ms * 1e-3) / 1e12
+        out = dict(
+            metric="QP solves/sec, 13-state N=10 SRBM MPC, batch=65536 at 1/2/4/8 MI355X",
+            value=total / (elapsed / args.steps), unit="QP/s", n_gpus=world, steps=args.steps,
+            warmup=args.warmup, ms_per_step=ms_per_step, higher_is_better=True,
+            scaling="weak", vs_baseline=None, dtype="f64",
+            data="synthetic (seeded SURVEY.md 8d TRON1 states x 16 gait candidates)",
+            config=dict(workload=f"TRON1 SRBM MPC {p['nx']}x{p['nu']} N={p['N']} "
+                                 f"({'box+friction' if p['constraints'] else 'box'}), "
+                                 f"linearise+discretise+condense+solve, batch {B} per GPU",
+                        batch_per_gpu=B, global_batch=total, horizon=p["N"], nx=p["nx"],
+                        nu=p["nu"], config=args.config, parallelism=f"dp{world}",
+                        solved_frac=solved, mean_solver_iters=float(iters.mean()),
+                        kernel_ms=dict(condense=cond_ms, solve=solve_ms)),
+            roofline=dict(bound="mfma", kernel=f"k_{dom}", achieved=achieved,
+                          peak=FP64_PEAK_TFLOPS, unit="TFLOP/s",
+                          frac=achieved / FP64_PEAK_TFLOPS, traffic=None,
+                          algorithmic_flops_per_qp=dom_flops / B,
+                          whole_step_tflops=(f_cond + f_solve) / (ms_per_step * 1e-3) / 1e12 / world
+                          * world),
+        )
+        if not args.no_cpu_baseline:
+            cb, _ = cpu_baseline(p, batch)
+            out["cpu_baseline"] = cb
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,157 @@
+/*
+ * mpcqp.h -- C ABI of the MI355X-native batched MPC-QP engine (libmpcqp.so).
+ *
+ * Drop-in boundary for the reference's per-tick control step
+ * (Fleming-Sung/mpc-limX-control: MPC -> mpcQP -> QPSolver).  Plain pointers and sizes only;
+ * every function returns an int status (MPCQP_OK == 0) and never prints or throws.
+ * All compute runs as HIP kernels on gfx950; there is no CPU fallback: without a usable
+ * device every compute entry point returns MPCQP_ERR_NO_DEVICE.
+ *
+ * Matrix layout: column-major (what Eigen's `.data()` hands out), unless stated otherwise.
+ *
+ * Entry point                     replaces (reference file:line)
+ * ------------------------------  ------------------------------------------------------------
+ * mpcqp_discretize                QPSolver::discretizeSystem   src/QPSolver.cpp:21-29
+ *                                 (declared include/QPSolver.h:19)
+ * mpcqp_build_qp                  QPSolver::buildQPParams      src/QPSolver.cpp:31-81
+ *                                 (declared include/QPSolver.h:22-25)
+ * mpcqp_solve_dense               QPSolver::solveQP            src/QPSolver.cpp:83-106
+ *                                 (qpOASES::QProblem::init + getPrimalSolution, :87-104;
+ *                                 declared include/QPSolver.h:28-31)
+ * mpcqp_plant_step                QPSolver::updateState        src/QPSolver.cpp:108-111
+ * mpcqp_ctx_create / _destroy     (new) owns device buffers + stream for the batched path
+ * mpcqp_batch_condense            mpcQP::buildSystemModel + QPSolver::discretizeSystem +
+ *                                 QPSolver::buildQPParams, batched (include/mpcQP.h:51-102,
+ *                                 121-182; src/QPSolver.cpp:21-81)
+ * mpcqp_batch_solve_qp            QPSolver::solveQP, batched (src/QPSolver.cpp:83-106)
+ * mpcqp_batch_solve               mpcQP::mpcQP ctor end to end (include/mpcQP.h:35-119),
+ *                                 i.e. the intended MPC::computeSupportFootForce
+ *                                 (include/MPCController.h:178-180), batched
+ * mpcqp_batch_select_min          (new) per-rank min-cost key for the multi-GPU selection
+ */
+#ifndef MPCQP_H
+#define MPCQP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------------------ */
+#define MPCQP_OK 0
+#define MPCQP_ERR_BAD_DIMS 1   /* dimensions outside the supported envelope            */
+#define MPCQP_ERR_INFEASIBLE 2 /* QP has no feasible point (qpOASES: RET_INIT_FAILED..)*/
+#define MPCQP_ERR_ITER_LIMIT 3 /* working-set iteration cap hit (qpOASES: nWSR)        */
+#define MPCQP_ERR_NOT_PD 4     /* reduced Hessian not positive definite                */
+#define MPCQP_ERR_DEVICE 5     /* HIP runtime error                                    */
+#define MPCQP_ERR_BAD_ARG 6    /* null pointer / invalid flag                          */
+#define MPCQP_ERR_NO_DEVICE 7  /* no HIP device visible                                */
+
+#define MPCQP_INFTY 1e20 /* qpOASES::INFTY as used at src/QPSolver.cpp:72-73 */
+
+/* ---- envelope ---------------------------------------------------------------------- */
+#define MPCQP_MAX_NX 32
+#define MPCQP_MAX_NU 16
+#define MPCQP_MAX_N 32
+#define MPCQP_MAX_NV 256   /* NU*N */
+#define MPCQP_MAX_FREE 64  /* free (lb < ub) variables per solve */
+
+/* layout flag of the dense constraint matrix handed to mpcqp_solve_dense */
+#define MPCQP_A_ROWMAJOR 0 /* qpOASES's convention (what QProblem::init expects)      */
+#define MPCQP_A_COLMAJOR 1 /* Eigen's storage (what the reference actually passes)    */
+
+/* ---- single-instance, reference-compatible entry points (run on the GPU, batch 1) ---- */
+int mpcqp_discretize(int nx, int nu, double Ts, const double *Ac, const double *Bc,
+                     double *Ad, double *Bd);
+
+/* Outputs use the reference's exact layouts and sizes (nV = nu*N):
+ *   H nV x nV, f nV, A_eq (nx*N) x nV, b_eq nx*N, lb/ub nV, A_ineq (2*nx*N) x nV,
+ *   lbA/ubA 2*nx*N (zero rows carry -/+MPCQP_INFTY).  Any output pointer may be NULL. */
+int mpcqp_build_qp(int nx, int nu, int N, const double *Ad, const double *Bd, const double *Q,
+                   const double *R, const double *P, const double *x_min, const double *x_max,
+                   double u_min, double u_max, const double *xi0, const double *xi_ref,
+                   double *H, double *f, double *A_eq, double *b_eq, double *lb, double *ub,
+                   double *A_ineq, double *lbA, double *ubA);
+
+/* min 1/2 x'Hx + f'x  s.t.  lb <= x <= ub,  lbA <= A x <= ubA  (rows with lbA == ubA are
+ * equalities; |bound| >= MPCQP_INFTY means absent).  Strictly convex only (H pos. def. on
+ * the free variables).  *nWSR: in = iteration cap (<= 0: default), out = iterations used.
+ * y (nullable, nV + nC): multipliers, qpOASES sign convention H x + f = y_b + A' y_A. */
+int mpcqp_solve_dense(int nV, int nC, const double *H, const double *f, const double *A,
+                      int a_layout, const double *lb, const double *ub, const double *lbA,
+                      const double *ubA, int *nWSR, double *x, double *y, double *cost);
+
+/* x <- Ad x + Bd u */
+int mpcqp_plant_step(int nx, int nu, const double *Ad, const double *Bd, double *x,
+                     const double *u);
+
+/* ---- batched engine ------------------------------------------------------------------ */
+#define MPCQP_MODEL_SRBM 0    /* convex-MPC single rigid body, 13 states, 6 inputs (2 feet) */
+#define MPCQP_MODEL_LITERAL 1 /* reference mpcQP::buildSystemModel, 13 states, 3 inputs    */
+#define MPCQP_CONS_BOX 0      /* per-foot force box from the contact schedule              */
+#define MPCQP_CONS_FRICTION 1 /* box + linearised friction pyramid |fx|,|fy| <= mu fz      */
+
+typedef struct mpcqp_model {
+    int nx, nu, N;           /* 13, 6 (SRBM) or 3 (LITERAL), horizon                         */
+    int model;               /* MPCQP_MODEL_*                                                */
+    int constraints;         /* MPCQP_CONS_*                                                 */
+    double Ts;               /* sample time (include/mpcQP.h:37: 0.001)                      */
+    double mass;             /* include/mpcQP.h:18: 9.585                                    */
+    double mu;               /* friction coefficient (MPCQP_CONS_FRICTION)                   */
+    double Ib[9];            /* body inertia, column-major (include/mpcQP.h:20-22)           */
+    double fz_min, fz_max;   /* per-foot normal force box when in contact                    */
+    double fxy_max;          /* per-foot tangential force box when in contact                */
+    double u_min, u_max;     /* LITERAL model input box (include/mpcQP.h:59-60)              */
+    const double *Q;         /* nx*nx state weight (host pointer, copied at create)          */
+    const double *R;         /* nu*nu input weight                                           */
+    const double *P;         /* nx*nx terminal weight                                        */
+    int max_iter;            /* solver iteration cap per instance (<= 0: default)            */
+    int max_free;            /* bound on free variables per instance (<= 0: nu*N)            */
+} mpcqp_model;
+
+/* Per-instance inputs (device pointers, instance-major = one contiguous record per QP):
+ *   x0      [B][nx]          initial state  [rpy, p, omega, v, g]      (include/mpcQP.h:66-71)
+ *   xref    [B][N+1][nx]     reference, column i = step i (Eigen col-major 13 x (N+1))
+ *   lin     [B][8]           SRBM: {yaw, r_L xyz, r_R xyz, 0}; LITERAL: {dx, dy, dz, ...}
+ *   contact [B]              uint64, bit 2k = left foot in contact at step k, 2k+1 = right
+ * Outputs (device pointers):
+ *   U [B][nu*N] (column-major nu x N: U_opt.col(0) = first nu entries), cost [B],
+ *   status [B] (MPCQP_* per instance), iters [B].                                          */
+typedef struct mpcqp_ctx mpcqp_ctx;
+
+int mpcqp_ctx_create(const mpcqp_model *model, int device, mpcqp_ctx **out);
+int mpcqp_ctx_destroy(mpcqp_ctx *ctx);
+/* stream: a hipStream_t to run on (NULL = the HIP null stream); a fresh context runs on a
+ * non-blocking stream of its own.  All batched calls are asynchronous on the context's
+ * stream; mpcqp_sync waits for it. */
+int mpcqp_set_stream(mpcqp_ctx *ctx, void *stream);
+int mpcqp_sync(mpcqp_ctx *ctx);
+
+int mpcqp_batch_condense(mpcqp_ctx *ctx, int B, const double *x0, const double *xref,
+                         const double *lin, double *H, double *f);
+int mpcqp_batch_solve_qp(mpcqp_ctx *ctx, int B, const double *H, const double *f,
+                         const uint64_t *contact, double *U, double *cost, int *status,
+                         int *iters);
+int mpcqp_batch_solve(mpcqp_ctx *ctx, int B, const double *x0, const double *xref,
+                      const double *lin, const uint64_t *contact, double *U, double *cost,
+                      int *status, int *iters);
+/* key = (order-preserving bits of (float)cost << 31) | (index_base + i), min over the batch,
+ * written to *key (device int64).  Instances with status != OK never win.  The caller
+ * reduces keys across ranks with one MIN all-reduce (RCCL). */
+int mpcqp_batch_select_min(mpcqp_ctx *ctx, int B, const double *cost, const int *status,
+                           int64_t index_base, int64_t *key);
+
+/* last kernel duration of the dominant kernel measured with HIP events on the ctx stream
+ * (ms; -1 if none) -- used by bench.py for the roofline figure */
+int mpcqp_enable_timing(mpcqp_ctx *ctx, int on);
+double mpcqp_last_kernel_ms(mpcqp_ctx *ctx, int which /* 0 condense, 1 solve, 2 fused */);
+
+const char *mpcqp_status_string(int status);
+int mpcqp_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCQP_H */

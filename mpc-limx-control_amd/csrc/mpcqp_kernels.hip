@@ -1,0 +1,663 @@
+// mpcqp_kernels.hip -- HIP kernels (gfx950) and the extern "C" implementation of
+// include/mpcqp.h.  One QP instance per 64-lane wavefront, one wavefront per workgroup.
+//
+// Kernels
+//   k_condense   linearise (SRBM / literal / given Ac,Bc) -> exp(M Ts) -> Phi_k = Ad^k Bd ->
+//                H, f (and, for the single-instance reference API, the reference's constraint
+//                arrays A_eq, b_eq, lb, ub, A_ineq, lbA, ubA).        src/QPSolver.cpp:21-81,
+//                include/mpcQP.h:121-182
+//   k_solve      corrected dense QP, Goldfarb-Idnani                  src/QPSolver.cpp:83-106
+//   k_select_min per-rank min-cost key (multi-GPU selection)
+//   k_plant      x <- Ad x + Bd u                                       src/QPSolver.cpp:108-111
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+
+#include "../../include/mpcqp.h"
+#include "condense.hpp"
+#include "gi_solver.hpp"
+
+using namespace mpcqp;
+
+namespace {
+
+struct CondenseArgs {
+    ModelConst mc;
+    int B;
+    const double *x0, *xref, *lin;   // [B][nx], [B][N+1][nx], [B][8]
+    const double *Ac, *Bc;           // generic model [B][nx*nx], [B][nx*nu]
+    const double *ABin;              // optional [B][nx*ns] = [Ad | Bd] (skip discretisation)
+    double *H, *f;                   // [B][nV*nV], [B][nV] (nullable when discretize_only)
+    double *ABout;                   // optional [B][nx*ns]
+    int discretize_only;
+    // reference-layout extras (single instance API)
+    const double *x_min, *x_max;
+    double u_min, u_max;
+    double *A_eq, *b_eq, *lb, *ub, *A_ineq, *lbA, *ubA;
+};
+
+size_t condense_lds_doubles(int nx, int nu, int N) {
+    const int ns = nx + nu, nV = nu * N;
+    const size_t ab = (size_t)nx * ns;
+    const size_t expm_ws = 8 * ab;  // T + 7 scratch
+    const size_t cond_ws = 3 * (size_t)nx * nV + 2 * (size_t)nx * (N + 1);
+    return ab + std::max(expm_ws, cond_ws);
+}
+
+__global__ void __launch_bounds__(64) k_condense(CondenseArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem_d[];
+    const int b = blockIdx.x;
+    if (b >= a.B) return;
+    const ModelConst &mc = a.mc;
+    const int nx = mc.nx, ns = mc.ns, nV = mc.nV, N = mc.N;
+    double *AB = smem_d;                 // [Ad | Bd]
+    double *ws = smem_d + nx * ns;       // scratch
+    if (a.ABin) {
+        for (int e = lane(); e < nx * ns; e += kWave) AB[e] = a.ABin[(size_t)b * nx * ns + e];
+        wave_sync();
+    } else {
+        double *T = ws;
+        double lin[8];
+        if (a.lin)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) lin[i] = a.lin[(size_t)b * 8 + i];
+        wave_build_model(mc, lin, a.Ac ? a.Ac + (size_t)b * nx * nx : nullptr,
+                         a.Bc ? a.Bc + (size_t)b * nx * mc.nu : nullptr, T);
+        wave_expm(nx, ns, T, ws + nx * ns, AB);
+    }
+    if (a.ABout)
+        for (int e = lane(); e < nx * ns; e += kWave) a.ABout[(size_t)b * nx * ns + e] = AB[e];
+    if (a.discretize_only) return;
+    double *Phi = nullptr, *xf = nullptr;
+    wave_condense(mc, AB, a.x0 + (size_t)b * nx, a.xref + (size_t)b * nx * (N + 1), ws,
+                  a.H + (size_t)b * nV * nV, a.f + (size_t)b * nV, &Phi, &xf);
+    // reference constraint arrays (src/QPSolver.cpp:63-80)
+    const int nu = mc.nu, NE = nx * N, NI = 2 * nx * N;
+    if (a.A_eq)
+        for (int e = lane(); e < NE * nV; e += kWave) {
+            const int r = e % NE, c = e / NE, m = r / nx + 1, i = r % nx, k = c / nu, cc = c % nu;
+            a.A_eq[(size_t)b * NE * nV + e] = (k < m) ? Phi[((m - 1 - k) * nu + cc) * nx + i] : 0.0;
+        }
+    if (a.b_eq)
+        for (int r = lane(); r < NE; r += kWave) a.b_eq[(size_t)b * NE + r] = xf[nx + r];
+    if (a.lb)
+        for (int r = lane(); r < nV; r += kWave) a.lb[(size_t)b * nV + r] = a.u_min;
+    if (a.ub)
+        for (int r = lane(); r < nV; r += kWave) a.ub[(size_t)b * nV + r] = a.u_max;
+    if (a.A_ineq)
+        for (int e = lane(); e < NI * nV; e += kWave) {
+            const int r = e % NI, c = e / NI, blk = r / nx;
+            double v = 0.0;
+            if ((blk & 1) == 0) {
+                const int m = blk / 2 + 1, i = r % nx, k = c / nu, cc = c % nu;
+                v = (k < m) ? Phi[((m - 1 - k) * nu + cc) * nx + i] : 0.0;
+            }
+            a.A_ineq[(size_t)b * NI * nV + e] = v;
+        }
+    if (a.lbA || a.ubA)
+        for (int r = lane(); r < NI; r += kWave) {
+            const int blk = r / nx, i = r % nx;
+            double lo = -kInfty, hi = kInfty;
+            if ((blk & 1) == 0) {
+                const double fr = xf[(blk / 2 + 1) * nx + i];
+                lo = a.x_min[i] - fr;
+                hi = a.x_max[i] - fr;
+            }
+            if (a.lbA) a.lbA[(size_t)b * NI + r] = lo;
+            if (a.ubA) a.ubA[(size_t)b * NI + r] = hi;
+        }
+}
+
+struct SolveArgs {
+    SolveProblem P;   // per-instance pointers are offsets from these bases
+    int B;
+    int nfmax;
+    const uint64_t *contact;  // [B] (gen_bounds) or nullptr
+    size_t a_stride;          // per-instance stride of A (0 = shared)
+    size_t ab_stride;         // per-instance stride of lbA/ubA (0 = shared)
+    double *x, *cost, *y;
+    int *status, *iters;
+};
+
+__global__ void __launch_bounds__(64) k_solve(SolveArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_b[];
+    const int b = blockIdx.x;
+    if (b >= a.B) return;
+    SolveProblem P = a.P;
+    const int nV = P.nV;
+    P.H += (size_t)b * nV * nV;
+    P.f += (size_t)b * nV;
+    if (P.lb) P.lb += (size_t)b * nV;
+    if (P.ub) P.ub += (size_t)b * nV;
+    if (P.A) P.A += (size_t)b * a.a_stride;
+    if (P.lbA) P.lbA += (size_t)b * a.ab_stride;
+    if (P.ubA) P.ubA += (size_t)b * a.ab_stride;
+    if (a.contact) P.contact = a.contact[b];
+    SolveOut O;
+    O.x = a.x + (size_t)b * nV;
+    O.cost = a.cost + b;
+    O.status = a.status + b;
+    O.iters = a.iters + b;
+    O.y = a.y ? a.y + (size_t)b * (nV + P.mA) : nullptr;
+    wave_gi_solve(P, O, smem_b, a.nfmax);
+}
+
+__device__ __forceinline__ unsigned long long order_bits(float c) {
+    const unsigned u = __float_as_uint(c);
+    return (u & 0x80000000u) ? (unsigned long long)(~u) : (unsigned long long)(u | 0x80000000u);
+}
+
+__global__ void __launch_bounds__(256) k_select_min(int B, const double *cost, const int *status,
+                                                     long long base, unsigned long long *key) {
+    __shared__ unsigned long long red[4];
+    unsigned long long best = 0x7fffffffffffffffull;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B; i += gridDim.x * blockDim.x) {
+        if (status[i] != 0) continue;
+        const unsigned long long k =
+            (order_bits((float)cost[i]) << 31) | ((unsigned long long)(base + i) & 0x7fffffffull);
+        best = k < best ? k : best;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long t = __shfl_xor(best, o, 64);
+        best = t < best ? t : best;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long m = red[0];
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) m = red[w] < m ? red[w] : m;
+        atomicMin(key, m);
+    }
+}
+
+__global__ void k_fill_u64(unsigned long long *p, unsigned long long v) { *p = v; }
+
+__global__ void __launch_bounds__(64) k_plant(int nx, int nu, const double *Ad, const double *Bd,
+                                              double *x, const double *u) {
+    __shared__ double xs[MPCQP_MAX_NX];
+    const int i = threadIdx.x;
+    if (i < nx) xs[i] = x[i];
+    __syncthreads();
+    if (i < nx) {
+        double s = 0.0, t = 0.0;
+        for (int l = 0; l < nx; ++l) s += Ad[l * nx + i] * xs[l];
+        for (int l = 0; l < nu; ++l) t += Bd[l * nx + i] * u[l];
+        x[i] = s + t;
+    }
+}
+
+// ------------------------------------------------------------------------------ host side
+void inv3(const double *A, double *Ai) {  // same formula as the oracle's model builder
+    const double a = A[0], b = A[3], c = A[6], d = A[1], e = A[4], f = A[7], g = A[2],
+                 h = A[5], i = A[8];
+    const double A00 = e * i - f * h, A01 = -(d * i - f * g), A02 = d * h - e * g;
+    const double det = a * A00 + b * A01 + c * A02;
+    const double id = 1.0 / det;
+    Ai[0] = A00 * id; Ai[3] = -(b * i - c * h) * id; Ai[6] = (b * f - c * e) * id;
+    Ai[1] = A01 * id; Ai[4] = (a * i - c * g) * id;  Ai[7] = -(a * f - c * d) * id;
+    Ai[2] = A02 * id; Ai[5] = -(a * h - b * g) * id; Ai[8] = (a * e - b * d) * id;
+}
+
+int hip_status(hipError_t e) { return e == hipSuccess ? MPCQP_OK : MPCQP_ERR_DEVICE; }
+
+#define HIP_TRY(x)                                \
+    do {                                          \
+        hipError_t e_ = (x);                      \
+        if (e_ != hipSuccess) { rc = MPCQP_ERR_DEVICE; goto out; } \
+    } while (0)
+
+bool have_device() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return false;
+    return n > 0;
+}
+
+// scoped device buffer list for the single-instance API
+struct DevBufs {
+    void *p[32];
+    int n = 0;
+    ~DevBufs() {
+        for (int i = 0; i < n; ++i) hipFree(p[i]);
+    }
+    template <class T>
+    T *alloc(size_t count) {
+        void *q = nullptr;
+        if (count == 0) count = 1;
+        if (hipMalloc(&q, count * sizeof(T)) != hipSuccess) return nullptr;
+        p[n++] = q;
+        return static_cast<T *>(q);
+    }
+    template <class T>
+    T *upload(const T *h, size_t count) {
+        if (!h) return nullptr;
+        T *d = alloc<T>(count);
+        if (d && hipMemcpy(d, h, count * sizeof(T), hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+        return d;
+    }
+};
+
+size_t set_lds(const void *kernel, size_t bytes) {
+    if (bytes > 64 * 1024)
+        hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    return bytes;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ context
+struct mpcqp_ctx {
+    mpcqp_model m;
+    int device;
+    double *dQ = nullptr, *dR = nullptr, *dP = nullptr;
+    double Ibinv[9];
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    bool timing = false;
+    hipEvent_t ev[6];
+    bool ev_ok = false;
+    bool ev_used[3] = {false, false, false};
+    double *scratchH = nullptr, *scratchF = nullptr;
+    size_t scratch_cap = 0;
+};
+
+extern "C" {
+
+const char *mpcqp_status_string(int s) {
+    switch (s) {
+        case MPCQP_OK: return "OK";
+        case MPCQP_ERR_BAD_DIMS: return "bad dimensions";
+        case MPCQP_ERR_INFEASIBLE: return "infeasible";
+        case MPCQP_ERR_ITER_LIMIT: return "iteration limit";
+        case MPCQP_ERR_NOT_PD: return "Hessian not positive definite";
+        case MPCQP_ERR_DEVICE: return "HIP device error";
+        case MPCQP_ERR_BAD_ARG: return "bad argument";
+        case MPCQP_ERR_NO_DEVICE: return "no HIP device";
+        default: return "unknown";
+    }
+}
+
+int mpcqp_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+static int check_dims(int nx, int nu, int N) {
+    if (nx <= 0 || nu <= 0 || N <= 0 || nx > MPCQP_MAX_NX || nu > MPCQP_MAX_NU || N > MPCQP_MAX_N ||
+        nu * N > MPCQP_MAX_NV)
+        return MPCQP_ERR_BAD_DIMS;
+    return MPCQP_OK;
+}
+
+static ModelConst make_mc(int nx, int nu, int N, int model, double Ts, double mass,
+                          const double *Ibinv, const double *Q, const double *R, const double *P) {
+    ModelConst mc;
+    mc.nx = nx; mc.nu = nu; mc.N = N; mc.nV = nu * N; mc.ns = nx + nu;
+    mc.model = model; mc.Ts = Ts; mc.mass = mass;
+    for (int i = 0; i < 9; ++i) mc.Ibinv[i] = Ibinv ? Ibinv[i] : 0.0;
+    mc.Q = Q; mc.R = R; mc.P = P;
+    return mc;
+}
+
+int mpcqp_discretize(int nx, int nu, double Ts, const double *Ac, const double *Bc, double *Ad,
+                     double *Bd) {
+    if (!Ac || !Bc || !Ad || !Bd) return MPCQP_ERR_BAD_ARG;
+    if (nx <= 0 || nu <= 0 || nx > MPCQP_MAX_NX || nu > MPCQP_MAX_NU) return MPCQP_ERR_BAD_DIMS;
+    if (!have_device()) return MPCQP_ERR_NO_DEVICE;
+    int rc = MPCQP_OK;
+    DevBufs bufs;
+    const int ns = nx + nu;
+    CondenseArgs a;
+    memset(&a, 0, sizeof(a));
+    a.mc = make_mc(nx, nu, 1, 2, Ts, 1.0, nullptr, nullptr, nullptr, nullptr);
+    a.B = 1;
+    a.Ac = bufs.upload(Ac, (size_t)nx * nx);
+    a.Bc = bufs.upload(Bc, (size_t)nx * nu);
+    a.ABout = bufs.alloc<double>((size_t)nx * ns);
+    a.discretize_only = 1;
+    if (!a.Ac || !a.Bc || !a.ABout) return MPCQP_ERR_DEVICE;
+    {
+        const size_t lds = set_lds((const void *)k_condense,
+                                   sizeof(double) * condense_lds_doubles(nx, nu, 1));
+        hipLaunchKernelGGL(k_condense, dim3(1), dim3(64), lds, 0, a);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpy(Ad, a.ABout, sizeof(double) * nx * nx, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(Bd, a.ABout + nx * nx, sizeof(double) * nx * nu, hipMemcpyDeviceToHost));
+    }
+out:
+    return rc;
+}
+
+int mpcqp_build_qp(int nx, int nu, int N, const double *Ad, const double *Bd, const double *Q,
+                   const double *R, const double *P, const double *x_min, const double *x_max,
+                   double u_min, double u_max, const double *xi0, const double *xi_ref,
+                   double *H, double *f, double *A_eq, double *b_eq, double *lb, double *ub,
+                   double *A_ineq, double *lbA, double *ubA) {
+    if (!Ad || !Bd || !Q || !R || !P || !xi0 || !xi_ref) return MPCQP_ERR_BAD_ARG;
+    if ((lbA || ubA) && (!x_min || !x_max)) return MPCQP_ERR_BAD_ARG;
+    int rc = check_dims(nx, nu, N);
+    if (rc) return rc;
+    if (!have_device()) return MPCQP_ERR_NO_DEVICE;
+    DevBufs bufs;
+    const int ns = nx + nu, nV = nu * N, NE = nx * N, NI = 2 * nx * N;
+    double *AB = (double *)malloc(sizeof(double) * nx * ns);
+    memcpy(AB, Ad, sizeof(double) * nx * nx);
+    memcpy(AB + nx * nx, Bd, sizeof(double) * nx * nu);
+    CondenseArgs a;
+    memset(&a, 0, sizeof(a));
+    const double *dQ = bufs.upload(Q, (size_t)nx * nx), *dR = bufs.upload(R, (size_t)nu * nu),
+                 *dP = bufs.upload(P, (size_t)nx * nx);
+    a.mc = make_mc(nx, nu, N, 2, 0.0, 1.0, nullptr, dQ, dR, dP);
+    a.B = 1;
+    a.ABin = bufs.upload(AB, (size_t)nx * ns);
+    free(AB);
+    a.x0 = bufs.upload(xi0, (size_t)nx);
+    a.xref = bufs.upload(xi_ref, (size_t)nx * (N + 1));
+    a.H = bufs.alloc<double>((size_t)nV * nV);
+    a.f = bufs.alloc<double>((size_t)nV);
+    a.x_min = bufs.upload(x_min, (size_t)nx);
+    a.x_max = bufs.upload(x_max, (size_t)nx);
+    a.u_min = u_min;
+    a.u_max = u_max;
+    a.A_eq = A_eq ? bufs.alloc<double>((size_t)NE * nV) : nullptr;
+    a.b_eq = b_eq ? bufs.alloc<double>((size_t)NE) : nullptr;
+    a.lb = lb ? bufs.alloc<double>((size_t)nV) : nullptr;
+    a.ub = ub ? bufs.alloc<double>((size_t)nV) : nullptr;
+    a.A_ineq = A_ineq ? bufs.alloc<double>((size_t)NI * nV) : nullptr;
+    a.lbA = lbA ? bufs.alloc<double>((size_t)NI) : nullptr;
+    a.ubA = ubA ? bufs.alloc<double>((size_t)NI) : nullptr;
+    if (!dQ || !dR || !dP || !a.ABin || !a.x0 || !a.xref || !a.H || !a.f) return MPCQP_ERR_DEVICE;
+    {
+        const size_t lds = set_lds((const void *)k_condense,
+                                   sizeof(double) * condense_lds_doubles(nx, nu, N));
+        hipLaunchKernelGGL(k_condense, dim3(1), dim3(64), lds, 0, a);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipDeviceSynchronize());
+        if (H) HIP_TRY(hipMemcpy(H, a.H, sizeof(double) * nV * nV, hipMemcpyDeviceToHost));
+        if (f) HIP_TRY(hipMemcpy(f, a.f, sizeof(double) * nV, hipMemcpyDeviceToHost));
+        if (A_eq) HIP_TRY(hipMemcpy(A_eq, a.A_eq, sizeof(double) * NE * nV, hipMemcpyDeviceToHost));
+        if (b_eq) HIP_TRY(hipMemcpy(b_eq, a.b_eq, sizeof(double) * NE, hipMemcpyDeviceToHost));
+        if (lb) HIP_TRY(hipMemcpy(lb, a.lb, sizeof(double) * nV, hipMemcpyDeviceToHost));
+        if (ub) HIP_TRY(hipMemcpy(ub, a.ub, sizeof(double) * nV, hipMemcpyDeviceToHost));
+        if (A_ineq) HIP_TRY(hipMemcpy(A_ineq, a.A_ineq, sizeof(double) * NI * nV, hipMemcpyDeviceToHost));
+        if (lbA) HIP_TRY(hipMemcpy(lbA, a.lbA, sizeof(double) * NI, hipMemcpyDeviceToHost));
+        if (ubA) HIP_TRY(hipMemcpy(ubA, a.ubA, sizeof(double) * NI, hipMemcpyDeviceToHost));
+    }
+out:
+    return rc;
+}
+
+int mpcqp_solve_dense(int nV, int nC, const double *H, const double *f, const double *A,
+                      int a_layout, const double *lb, const double *ub, const double *lbA,
+                      const double *ubA, int *nWSR, double *x, double *y, double *cost) {
+    if (!H || !f || !x || (nC > 0 && !A)) return MPCQP_ERR_BAD_ARG;
+    if (a_layout != MPCQP_A_ROWMAJOR && a_layout != MPCQP_A_COLMAJOR) return MPCQP_ERR_BAD_ARG;
+    if (nV <= 0 || nV > MPCQP_MAX_NV || nC < 0 || nC > 4096) return MPCQP_ERR_BAD_DIMS;
+    if (!have_device()) return MPCQP_ERR_NO_DEVICE;
+    int rc = MPCQP_OK;
+    DevBufs bufs;
+    // free-variable count decides the LDS size; fixed variables (lb == ub) are eliminated
+    int nfree = 0;
+    for (int i = 0; i < nV; ++i) {
+        const double lo = lb ? lb[i] : -MPCQP_INFTY, hi = ub ? ub[i] : MPCQP_INFTY;
+        if (lo != hi) ++nfree;
+    }
+    if (nfree > MPCQP_MAX_FREE) return MPCQP_ERR_BAD_DIMS;
+    const int nfmax = std::max(1, nfree);
+    SolveArgs a;
+    memset(&a, 0, sizeof(a));
+    a.B = 1;
+    a.nfmax = nfmax;
+    a.P.nV = nV;
+    a.P.H = bufs.upload(H, (size_t)nV * nV);
+    a.P.f = bufs.upload(f, (size_t)nV);
+    a.P.lb = bufs.upload(lb, (size_t)nV);
+    a.P.ub = bufs.upload(ub, (size_t)nV);
+    a.P.mA = nC;
+    a.P.A = nC ? bufs.upload(A, (size_t)nC * nV) : nullptr;
+    a.P.a_colmajor = a_layout == MPCQP_A_COLMAJOR;
+    a.P.lbA = nC ? bufs.upload(lbA, (size_t)nC) : nullptr;
+    a.P.ubA = nC ? bufs.upload(ubA, (size_t)nC) : nullptr;
+    a.P.max_iter = (nWSR && *nWSR > 0) ? *nWSR : 0;
+    double *dx = bufs.alloc<double>(nV), *dc = bufs.alloc<double>(1);
+    int *ds = bufs.alloc<int>(1), *di = bufs.alloc<int>(1);
+    double *dy = y ? bufs.alloc<double>((size_t)nV + nC) : nullptr;
+    a.x = dx; a.cost = dc; a.status = ds; a.iters = di; a.y = dy;
+    if (!a.P.H || !a.P.f || !dx || !dc || !ds || !di) return MPCQP_ERR_DEVICE;
+    if (nC && (!a.P.A)) return MPCQP_ERR_DEVICE;
+    {
+        const size_t lds = set_lds((const void *)k_solve, gi_lds_bytes(nfmax, nV, nC, 0));
+        int st = 0, it = 0;
+        double c = 0.0;
+        hipLaunchKernelGGL(k_solve, dim3(1), dim3(64), lds, 0, a);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpy(x, dx, sizeof(double) * nV, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(&st, ds, sizeof(int), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(&it, di, sizeof(int), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(&c, dc, sizeof(double), hipMemcpyDeviceToHost));
+        if (y) HIP_TRY(hipMemcpy(y, dy, sizeof(double) * (nV + nC), hipMemcpyDeviceToHost));
+        if (nWSR) *nWSR = it;
+        if (cost) *cost = c;
+        rc = st;
+    }
+out:
+    return rc;
+}
+
+int mpcqp_plant_step(int nx, int nu, const double *Ad, const double *Bd, double *x,
+                     const double *u) {
+    if (!Ad || !Bd || !x || !u) return MPCQP_ERR_BAD_ARG;
+    if (nx <= 0 || nu <= 0 || nx > MPCQP_MAX_NX || nu > MPCQP_MAX_NU) return MPCQP_ERR_BAD_DIMS;
+    if (!have_device()) return MPCQP_ERR_NO_DEVICE;
+    int rc = MPCQP_OK;
+    DevBufs bufs;
+    const double *dA = bufs.upload(Ad, (size_t)nx * nx), *dB = bufs.upload(Bd, (size_t)nx * nu),
+                 *du = bufs.upload(u, (size_t)nu);
+    double *dx = bufs.upload(x, (size_t)nx);
+    if (!dA || !dB || !du || !dx) return MPCQP_ERR_DEVICE;
+    hipLaunchKernelGGL(k_plant, dim3(1), dim3(64), 0, 0, nx, nu, dA, dB, dx, du);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(x, dx, sizeof(double) * nx, hipMemcpyDeviceToHost));
+out:
+    return rc;
+}
+
+// ------------------------------------------------------------------------- batched path
+int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
+    if (!m || !out || !m->Q || !m->R || !m->P) return MPCQP_ERR_BAD_ARG;
+    *out = nullptr;
+    int rc = check_dims(m->nx, m->nu, m->N);
+    if (rc) return rc;
+    if (m->model == MPCQP_MODEL_SRBM && (m->nx != 13 || m->nu != 6)) return MPCQP_ERR_BAD_DIMS;
+    if (m->model == MPCQP_MODEL_LITERAL && (m->nx != 13 || m->nu != 3)) return MPCQP_ERR_BAD_DIMS;
+    if (m->model != MPCQP_MODEL_SRBM && m->model != MPCQP_MODEL_LITERAL) return MPCQP_ERR_BAD_ARG;
+    if (m->constraints != MPCQP_CONS_BOX && m->constraints != MPCQP_CONS_FRICTION)
+        return MPCQP_ERR_BAD_ARG;
+    const int nfmax = m->max_free > 0 ? m->max_free : m->nu * m->N;
+    if (nfmax > MPCQP_MAX_FREE) return MPCQP_ERR_BAD_DIMS;
+    if (!have_device()) return MPCQP_ERR_NO_DEVICE;
+    if (hipSetDevice(device) != hipSuccess) return MPCQP_ERR_DEVICE;
+    mpcqp_ctx *c = new (std::nothrow) mpcqp_ctx();
+    if (!c) return MPCQP_ERR_DEVICE;
+    c->m = *m;
+    c->device = device;
+    inv3(m->Ib, c->Ibinv);
+    const int nx = m->nx, nu = m->nu;
+    if (hipMalloc(&c->dQ, sizeof(double) * nx * nx) != hipSuccess ||
+        hipMalloc(&c->dR, sizeof(double) * nu * nu) != hipSuccess ||
+        hipMalloc(&c->dP, sizeof(double) * nx * nx) != hipSuccess ||
+        hipMemcpy(c->dQ, m->Q, sizeof(double) * nx * nx, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->dR, m->R, sizeof(double) * nu * nu, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->dP, m->P, sizeof(double) * nx * nx, hipMemcpyHostToDevice) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        mpcqp_ctx_destroy(c);
+        return MPCQP_ERR_DEVICE;
+    }
+    c->own_stream = true;
+    c->m.Q = c->m.R = c->m.P = nullptr;  // host pointers are not kept
+    c->ev_ok = true;
+    for (int i = 0; i < 6; ++i)
+        if (hipEventCreate(&c->ev[i]) != hipSuccess) c->ev_ok = false;
+    *out = c;
+    return MPCQP_OK;
+}
+
+int mpcqp_ctx_destroy(mpcqp_ctx *c) {
+    if (!c) return MPCQP_ERR_BAD_ARG;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    hipFree(c->dQ);
+    hipFree(c->dR);
+    hipFree(c->dP);
+    hipFree(c->scratchH);
+    hipFree(c->scratchF);
+    if (c->ev_ok)
+        for (int i = 0; i < 6; ++i) hipEventDestroy(c->ev[i]);
+    if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return MPCQP_OK;
+}
+
+int mpcqp_set_stream(mpcqp_ctx *c, void *stream) {
+    if (!c) return MPCQP_ERR_BAD_ARG;
+    if (c->own_stream && c->stream) {
+        hipStreamSynchronize(c->stream);
+        hipStreamDestroy(c->stream);
+    }
+    c->own_stream = false;
+    c->stream = (hipStream_t)stream;  // NULL = the HIP null stream
+    return MPCQP_OK;
+}
+
+int mpcqp_sync(mpcqp_ctx *c) {
+    if (!c) return MPCQP_ERR_BAD_ARG;
+    return hip_status(hipStreamSynchronize(c->stream));
+}
+
+int mpcqp_enable_timing(mpcqp_ctx *c, int on) {
+    if (!c) return MPCQP_ERR_BAD_ARG;
+    c->timing = on && c->ev_ok;
+    return MPCQP_OK;
+}
+
+double mpcqp_last_kernel_ms(mpcqp_ctx *c, int which) {
+    if (!c || which < 0 || which > 2 || !c->ev_used[which]) return -1.0;
+    float ms = -1.0f;
+    if (hipEventSynchronize(c->ev[2 * which + 1]) != hipSuccess) return -1.0;
+    if (hipEventElapsedTime(&ms, c->ev[2 * which], c->ev[2 * which + 1]) != hipSuccess) return -1.0;
+    return ms;
+}
+
+static CondenseArgs batch_condense_args(mpcqp_ctx *c, int B, const double *x0, const double *xref,
+                                        const double *lin, double *H, double *f) {
+    CondenseArgs a;
+    memset(&a, 0, sizeof(a));
+    a.mc = make_mc(c->m.nx, c->m.nu, c->m.N, c->m.model, c->m.Ts, c->m.mass, c->Ibinv, c->dQ,
+                   c->dR, c->dP);
+    a.B = B;
+    a.x0 = x0;
+    a.xref = xref;
+    a.lin = lin;
+    a.H = H;
+    a.f = f;
+    return a;
+}
+
+int mpcqp_batch_condense(mpcqp_ctx *c, int B, const double *x0, const double *xref,
+                         const double *lin, double *H, double *f) {
+    if (!c || !x0 || !xref || !lin || !H || !f || B < 0) return MPCQP_ERR_BAD_ARG;
+    if (B == 0) return MPCQP_OK;
+    hipSetDevice(c->device);
+    CondenseArgs a = batch_condense_args(c, B, x0, xref, lin, H, f);
+    const size_t lds = set_lds((const void *)k_condense,
+                               sizeof(double) * condense_lds_doubles(c->m.nx, c->m.nu, c->m.N));
+    if (c->timing) hipEventRecord(c->ev[0], c->stream);
+    hipLaunchKernelGGL(k_condense, dim3(B), dim3(64), lds, c->stream, a);
+    if (c->timing) { hipEventRecord(c->ev[1], c->stream); c->ev_used[0] = true; }
+    return hip_status(hipGetLastError());
+}
+
+int mpcqp_batch_solve_qp(mpcqp_ctx *c, int B, const double *H, const double *f,
+                         const uint64_t *contact, double *U, double *cost, int *status,
+                         int *iters) {
+    if (!c || !H || !f || !U || !cost || !status || !iters || B < 0) return MPCQP_ERR_BAD_ARG;
+    if (c->m.model == MPCQP_MODEL_SRBM && !contact) return MPCQP_ERR_BAD_ARG;
+    if (B == 0) return MPCQP_OK;
+    hipSetDevice(c->device);
+    SolveArgs a;
+    memset(&a, 0, sizeof(a));
+    const mpcqp_model &m = c->m;
+    a.B = B;
+    a.nfmax = m.max_free > 0 ? m.max_free : m.nu * m.N;
+    a.P.nV = m.nu * m.N;
+    a.P.H = H;
+    a.P.f = f;
+    a.P.gen_bounds = 1;
+    a.P.model = m.model;
+    a.P.nu = m.nu;
+    a.P.N = m.N;
+    a.P.nfeet = 2;
+    a.P.fz_min = m.fz_min;
+    a.P.fz_max = m.fz_max;
+    a.P.fxy_max = m.fxy_max;
+    a.P.u_min = m.u_min;
+    a.P.u_max = m.u_max;
+    a.P.friction = (m.model == MPCQP_MODEL_SRBM && m.constraints == MPCQP_CONS_FRICTION);
+    a.P.mu = m.mu;
+    a.P.max_iter = m.max_iter;
+    a.contact = (m.model == MPCQP_MODEL_SRBM) ? contact : nullptr;
+    a.x = U;
+    a.cost = cost;
+    a.status = status;
+    a.iters = iters;
+    const int nfric = a.P.friction ? 4 * m.N * 2 : 0;
+    const size_t lds = set_lds((const void *)k_solve, gi_lds_bytes(a.nfmax, a.P.nV, 0, nfric));
+    if (c->timing) hipEventRecord(c->ev[2], c->stream);
+    hipLaunchKernelGGL(k_solve, dim3(B), dim3(64), lds, c->stream, a);
+    if (c->timing) { hipEventRecord(c->ev[3], c->stream); c->ev_used[1] = true; }
+    return hip_status(hipGetLastError());
+}
+
+int mpcqp_batch_solve(mpcqp_ctx *c, int B, const double *x0, const double *xref,
+                      const double *lin, const uint64_t *contact, double *U, double *cost,
+                      int *status, int *iters) {
+    if (!c) return MPCQP_ERR_BAD_ARG;
+    if (B <= 0) return B == 0 ? MPCQP_OK : MPCQP_ERR_BAD_ARG;
+    hipSetDevice(c->device);
+    const size_t nV = (size_t)c->m.nu * c->m.N;
+    if (c->scratch_cap < (size_t)B) {
+        hipFree(c->scratchH);
+        hipFree(c->scratchF);
+        c->scratchH = c->scratchF = nullptr;
+        c->scratch_cap = 0;
+        if (hipMalloc(&c->scratchH, sizeof(double) * nV * nV * B) != hipSuccess ||
+            hipMalloc(&c->scratchF, sizeof(double) * nV * B) != hipSuccess)
+            return MPCQP_ERR_DEVICE;
+        c->scratch_cap = B;
+    }
+    int rc = mpcqp_batch_condense(c, B, x0, xref, lin, c->scratchH, c->scratchF);
+    if (rc) return rc;
+    return mpcqp_batch_solve_qp(c, B, c->scratchH, c->scratchF, contact, U, cost, status, iters);
+}
+
+int mpcqp_batch_select_min(mpcqp_ctx *c, int B, const double *cost, const int *status,
+                           int64_t index_base, int64_t *key) {
+    if (!c || !cost || !status || !key || B < 0) return MPCQP_ERR_BAD_ARG;
+    hipSetDevice(c->device);
+    unsigned long long *k = reinterpret_cast<unsigned long long *>(key);
+    hipLaunchKernelGGL(k_fill_u64, dim3(1), dim3(1), 0, c->stream, k, 0x7fffffffffffffffull);
+    if (B > 0) {
+        const int blocks = std::min(1024, (B + 255) / 256);
+        hipLaunchKernelGGL(k_select_min, dim3(blocks), dim3(256), 0, c->stream, B, cost, status,
+                           (long long)index_base, k);
+    }
+    return hip_status(hipGetLastError());
+}
+
+}  // extern "C"

@@ -1,0 +1,61 @@
+// wave_ops.hpp -- 64-lane wavefront primitives for the one-QP-per-wavefront kernels (gfx950).
+//
+// Every kernel in this library runs one problem instance per 64-lane wavefront (one wave per
+// workgroup), so all control flow inside an instance is wave-uniform and these helpers can
+// assume a full, converged wave.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mpcqp {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane() { return (int)__lane_id(); }
+
+// Broadcast lane `src` (wave-uniform index) of a double to the whole wave (v_readlane x2).
+__device__ __forceinline__ double readlane(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), src);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ int readlane(int v, int src) {
+    return __builtin_amdgcn_readlane(v, src);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
+    return v;
+}
+// lexicographic (value, index) minimum; lanes with nothing to offer pass (+inf, INT_MAX)
+__device__ __forceinline__ void wave_argmin(double &v, int &idx) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(v, o, kWave);
+        const int oi = __shfl_xor(idx, o, kWave);
+        if (ov < v || (ov == v && oi < idx)) { v = ov; idx = oi; }
+    }
+}
+// (value, index) maximum with the lowest index winning ties (Eigen maxCoeff semantics)
+__device__ __forceinline__ void wave_argmax(double &v, int &idx) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(v, o, kWave);
+        const int oi = __shfl_xor(idx, o, kWave);
+        if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
+    }
+}
+
+// Compiler + LDS ordering point between phases of a single-wave workgroup.  With a 64-thread
+// workgroup the backend drops the s_barrier itself; the workgroup fence keeps LDS stores of
+// one lane ordered before loads of another.
+__device__ __forceinline__ void wave_sync() { __syncthreads(); }
+
+}  // namespace mpcqp

@@ -1,0 +1,86 @@
+"""ctypes binding of libmpcqp.so (include/mpcqp.h).
+
+The library is the product: HIP kernels for gfx950 behind a C ABI.  There is no Python or
+CPU fallback -- if the library is missing, importing the engine raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libmpcqp.so")
+
+MPCQP_OK = 0
+STATUS = {0: "OK", 1: "BAD_DIMS", 2: "INFEASIBLE", 3: "ITER_LIMIT", 4: "NOT_PD", 5: "DEVICE",
+          6: "BAD_ARG", 7: "NO_DEVICE"}
+MPCQP_INFTY = 1e20
+MODEL_SRBM, MODEL_LITERAL = 0, 1
+CONS_BOX, CONS_FRICTION = 0, 1
+A_ROWMAJOR, A_COLMAJOR = 0, 1
+
+EXPORTS = [
+    "mpcqp_discretize", "mpcqp_build_qp", "mpcqp_solve_dense", "mpcqp_plant_step",
+    "mpcqp_ctx_create", "mpcqp_ctx_destroy", "mpcqp_set_stream", "mpcqp_sync",
+    "mpcqp_batch_condense", "mpcqp_batch_solve_qp", "mpcqp_batch_solve",
+    "mpcqp_batch_select_min", "mpcqp_enable_timing", "mpcqp_last_kernel_ms",
+    "mpcqp_status_string", "mpcqp_device_count",
+]
+
+
+class MpcqpError(RuntimeError):
+    def __init__(self, fn, code):
+        super().__init__(f"{fn} failed: {STATUS.get(code, code)} ({code})")
+        self.code = code
+
+
+class Model(C.Structure):
+    """mirror of struct mpcqp_model"""
+    _fields_ = [("nx", C.c_int), ("nu", C.c_int), ("N", C.c_int), ("model", C.c_int),
+                ("constraints", C.c_int), ("Ts", C.c_double), ("mass", C.c_double),
+                ("mu", C.c_double), ("Ib", C.c_double * 9), ("fz_min", C.c_double),
+                ("fz_max", C.c_double), ("fxy_max", C.c_double), ("u_min", C.c_double),
+                ("u_max", C.c_double), ("Q", C.c_void_p), ("R", C.c_void_p),
+                ("P", C.c_void_p), ("max_iter", C.c_int), ("max_free", C.c_int)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libmpcqp.so; raise loudly if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libmpcqp.so not built ({LIB_PATH}); run `make -C mpc-limx-control_amd` "
+                          "or __graft_entry__.build()")
+    L = C.CDLL(LIB_PATH)
+    vp, dp, ip, i = C.c_void_p, C.c_void_p, C.c_void_p, C.c_int
+    d = C.c_double
+    L.mpcqp_discretize.argtypes = [i, i, d, vp, vp, vp, vp]
+    L.mpcqp_build_qp.argtypes = [i, i, i] + [vp] * 7 + [d, d] + [vp] * 11
+    L.mpcqp_solve_dense.argtypes = [i, i, vp, vp, vp, i, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.mpcqp_plant_step.argtypes = [i, i, vp, vp, vp, vp]
+    L.mpcqp_ctx_create.argtypes = [C.POINTER(Model), i, C.POINTER(vp)]
+    L.mpcqp_ctx_destroy.argtypes = [vp]
+    L.mpcqp_set_stream.argtypes = [vp, vp]
+    L.mpcqp_sync.argtypes = [vp]
+    L.mpcqp_batch_condense.argtypes = [vp, i, vp, vp, vp, vp, vp]
+    L.mpcqp_batch_solve_qp.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp]
+    L.mpcqp_batch_solve.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.mpcqp_batch_select_min.argtypes = [vp, i, vp, vp, C.c_int64, vp]
+    L.mpcqp_enable_timing.argtypes = [vp, i]
+    L.mpcqp_last_kernel_ms.argtypes = [vp, i]
+    L.mpcqp_last_kernel_ms.restype = C.c_double
+    L.mpcqp_status_string.argtypes = [i]
+    L.mpcqp_status_string.restype = C.c_char_p
+    L.mpcqp_device_count.argtypes = []
+    _lib = L
+    return L
+
+
+def check(fn, code):
+    if code != MPCQP_OK:
+        raise MpcqpError(fn, code)
+    return code

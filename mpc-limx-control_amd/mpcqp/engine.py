@@ -1,0 +1,119 @@
+"""Batched engine: device-resident inputs/outputs (torch tensors for HBM allocation and
+streams -- plumbing only) driven through the C ABI of libmpcqp.so.
+
+Mirrors the reference's per-tick step (mpcQP ctor, include/mpcQP.h:35-119: linearise ->
+discretise -> condense -> solve -> U_opt.col(0)) for a whole batch of states x gait candidates.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import model as _model
+from ._lib import check, lib
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class BatchEngine:
+    """One mpcqp_ctx on one GPU.  Arrays are torch tensors on `device`."""
+
+    def __init__(self, params: dict, device: int = 0, stream=None):
+        import torch  # plumbing: device memory + streams
+
+        self.torch = torch
+        self.p = params
+        self.device = device
+        self.nV = params["nu"] * params["N"]
+        m, keep = _model.to_struct(params)
+        ctx = C.c_void_p()
+        check("mpcqp_ctx_create", lib().mpcqp_ctx_create(C.byref(m), device, C.byref(ctx)))
+        del keep
+        self.ctx = ctx
+        if stream is None:  # share torch's stream so uploads/memsets are ordered before us
+            stream = torch.cuda.current_stream(device).cuda_stream
+        check("mpcqp_set_stream", lib().mpcqp_set_stream(self.ctx, C.c_void_p(stream)))
+
+    def close(self):
+        if self.ctx:
+            lib().mpcqp_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- buffers ---------------------------------------------------------------------------
+    def upload(self, batch: dict):
+        t = self.torch
+        dev = f"cuda:{self.device}"
+        out = {k: t.from_numpy(np.ascontiguousarray(batch[k])).to(dev)
+               for k in ("x0", "xref", "lin")}
+        out["contact"] = t.from_numpy(batch["contact"].view(np.int64)).to(dev)
+        B = batch["x0"].shape[0]
+        out["U"] = t.zeros((B, self.nV), dtype=t.float64, device=dev)
+        out["cost"] = t.zeros(B, dtype=t.float64, device=dev)
+        out["status"] = t.zeros(B, dtype=t.int32, device=dev)
+        out["iters"] = t.zeros(B, dtype=t.int32, device=dev)
+        out["key"] = t.zeros(1, dtype=t.int64, device=dev)
+        out["B"] = B
+        return out
+
+    # -- stages ----------------------------------------------------------------------------
+    def condense(self, d, H=None, f=None):
+        t = self.torch
+        B = d["B"]
+        if H is None:
+            H = t.empty((B, self.nV, self.nV), dtype=t.float64, device=d["x0"].device)
+            f = t.empty((B, self.nV), dtype=t.float64, device=d["x0"].device)
+        check("mpcqp_batch_condense", lib().mpcqp_batch_condense(
+            self.ctx, B, _ptr(d["x0"]), _ptr(d["xref"]), _ptr(d["lin"]), _ptr(H), _ptr(f)))
+        return H, f
+
+    def solve_qp(self, d, H, f):
+        check("mpcqp_batch_solve_qp", lib().mpcqp_batch_solve_qp(
+            self.ctx, d["B"], _ptr(H), _ptr(f), _ptr(d["contact"]), _ptr(d["U"]),
+            _ptr(d["cost"]), _ptr(d["status"]), _ptr(d["iters"])))
+
+    def solve(self, d):
+        """linearise + discretise + condense + solve, all on device (async on the ctx stream)"""
+        check("mpcqp_batch_solve", lib().mpcqp_batch_solve(
+            self.ctx, d["B"], _ptr(d["x0"]), _ptr(d["xref"]), _ptr(d["lin"]),
+            _ptr(d["contact"]), _ptr(d["U"]), _ptr(d["cost"]), _ptr(d["status"]),
+            _ptr(d["iters"])))
+
+    def select_min(self, d, index_base: int = 0):
+        check("mpcqp_batch_select_min", lib().mpcqp_batch_select_min(
+            self.ctx, d["B"], _ptr(d["cost"]), _ptr(d["status"]), int(index_base),
+            _ptr(d["key"])))
+        return d["key"]
+
+    def sync(self):
+        check("mpcqp_sync", lib().mpcqp_sync(self.ctx))
+
+    def enable_timing(self, on=True):
+        lib().mpcqp_enable_timing(self.ctx, 1 if on else 0)
+
+    def last_kernel_ms(self, which: int) -> float:
+        return float(lib().mpcqp_last_kernel_ms(self.ctx, which))
+
+
+def decode_key(key: int):
+    """(float32 cost, global index) from a select_min key"""
+    idx = key & 0x7FFFFFFF
+    ob = (key >> 31) & 0xFFFFFFFF
+    bits = (ob & 0x7FFFFFFF) if (ob & 0x80000000) else (~ob & 0xFFFFFFFF)
+    cost = np.frombuffer(np.uint32(bits).tobytes(), dtype=np.float32)[0]
+    return float(cost), int(idx)
+
+
+def encode_key(cost: float, index: int) -> int:
+    """host restatement of the device key (for the CPU reference of the selection)"""
+    u = int(np.frombuffer(np.float32(cost).tobytes(), dtype=np.uint32)[0])
+    ob = (~u & 0xFFFFFFFF) if (u & 0x80000000) else (u | 0x80000000)
+    return (ob << 31) | (index & 0x7FFFFFFF)

@@ -1,0 +1,99 @@
+"""Seeded synthetic per-instance inputs.
+
+Batch = S states x C candidate gait phases.  Per state:
+  roll, pitch ~ U(-0.1, 0.1); yaw ~ U(-pi, pi); x, y ~ U(-1, 1); z ~ U(0.76, 0.86);
+  omega ~ N(0, 0.2); vx ~ U(-1, 1); vy ~ U(-0.3, 0.3); vz ~ N(0, 0.05); g = -9.8
+  foot lever arms r_s = Rz(yaw) (static offset_s + N(0, 0.03))  (world frame, foot - CoM)
+  xref as include/mpcQP.h:77-97 (yaw rate 0.1) with a per-state forward speed ~ U(0, 1)
+Per candidate: gait phase offset ~ U(0, 1 s); contact per horizon step from
+MPC::calculateGait (include/MPCController.h:61-75).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from .model import GRAVITY, STANCE_TIME, SWING_TIME, static_foot_offsets
+
+DEFAULT_SEED = 20250404
+
+
+def gait_contact_mask(N: int, Ts: float, phase0: float, swing=SWING_TIME, stance=STANCE_TIME) -> int:
+    """bit 2k = left foot in contact at step k, bit 2k+1 = right (calculateGait per step)."""
+    cycle = float(np.float32(swing) + np.float32(stance))
+    mask = 0
+    for k in range(N):
+        ph = math.fmod(phase0 + float(k) * Ts, cycle)
+        mask |= (1 << (2 * k + 1)) if ph < float(swing) else (1 << (2 * k))
+    return mask
+
+
+def make_batch(p: dict, B: int, seed: int = DEFAULT_SEED, candidates: int = 16):
+    """-> dict(x0 [B,13], xref [B,N+1,13], lin [B,8], contact [B] uint64)"""
+    rng = np.random.default_rng(seed)
+    N, nx, Ts = p["N"], p["nx"], p["Ts"]
+    C = max(1, min(candidates, B))
+    S = (B + C - 1) // C
+    roll = rng.uniform(-0.1, 0.1, S)
+    pitch = rng.uniform(-0.1, 0.1, S)
+    yaw = rng.uniform(-math.pi, math.pi, S)
+    pos = np.stack([rng.uniform(-1, 1, S), rng.uniform(-1, 1, S), rng.uniform(0.76, 0.86, S)], 1)
+    om = rng.normal(0.0, 0.2, (S, 3))
+    vel = np.stack([rng.uniform(-1, 1, S), rng.uniform(-0.3, 0.3, S), rng.normal(0, 0.05, S)], 1)
+    vxr = rng.uniform(0.0, 1.0, S)
+    off_l, off_r = static_foot_offsets()
+    nl = rng.normal(0.0, 0.03, (S, 3))
+    nr = rng.normal(0.0, 0.03, (S, 3))
+    phase = rng.uniform(0.0, 1.0, (S, C))
+
+    x0 = np.zeros((S, nx))
+    x0[:, 0], x0[:, 1], x0[:, 2] = roll, pitch, yaw
+    x0[:, 3:6] = pos
+    x0[:, 6:9] = om
+    x0[:, 9:12] = vel
+    x0[:, 12] = -GRAVITY
+    # reference trajectory, include/mpcQP.h:77-97
+    t = np.arange(N + 1) * Ts
+    xref = np.repeat(x0[:, None, :], N + 1, axis=1)
+    xref[:, :, 2] = yaw[:, None] + t[None, :] * 0.1
+    xref[:, :, 3] = pos[:, 0:1] + t[None, :] * vxr[:, None]
+    xref[:, 1:, 9] = vxr[:, None]
+    # lever arms
+    cy, sy = np.cos(yaw), np.sin(yaw)
+    lin = np.zeros((S, 8))
+    lin[:, 0] = yaw
+    for j, (off, nz) in enumerate(((off_l, nl), (off_r, nr))):
+        o = off[None, :] + nz
+        lin[:, 1 + 3 * j] = cy * o[:, 0] - sy * o[:, 1]
+        lin[:, 2 + 3 * j] = sy * o[:, 0] + cy * o[:, 1]
+        lin[:, 3 + 3 * j] = o[:, 2]
+    if p["model"] == 1:  # literal model: lin = support-foot offset (dx, dy, dz)
+        lit = np.zeros((S, 8))
+        lit[:, 0:3] = lin[:, 1:4]
+        lin = lit
+    contact = np.array([[gait_contact_mask(N, Ts, float(phase[s, c])) for c in range(C)]
+                        for s in range(S)], dtype=np.uint64)
+    rep = lambda a: np.repeat(a, C, axis=0)[:B]
+    return dict(x0=np.ascontiguousarray(rep(x0)), xref=np.ascontiguousarray(rep(xref)),
+                lin=np.ascontiguousarray(rep(lin)), contact=np.ascontiguousarray(contact.reshape(-1)[:B]))
+
+
+def qp_harness_inputs(k: int = 0):
+    """The reference's qp_test plant and tick-k circle reference (src/qpSolver_test.cpp:6-50)."""
+    Ts, N = 0.01, 15
+    Ac = np.array([[0, 1, 0, 0], [0, -0.1, 0, 0], [0, 0, 0, 1], [0, 0, 0, -0.1]], float)
+    Bc = np.array([[0, 0], [5, 0], [0, 0], [0, 5]], float)
+    Q = np.diag([50.0, 5.0, 50.0, 5.0])
+    R = 0.1 * np.eye(2)
+    P = 20 * Q
+    x_min = np.array([-5.0, -3.0, -5.0, -3.0])
+    xr = np.zeros((4, N + 1))
+    for i in range(N + 1):
+        th = 0.5 * (k * Ts + i * Ts)
+        xr[0, i] = 2.0 * math.cos(th)
+        xr[2, i] = 2.0 * math.sin(th)
+        xr[1, i] = -2.0 * 0.5 * math.sin(th)
+        xr[3, i] = 2.0 * 0.5 * math.cos(th)
+    return dict(Ts=Ts, N=N, Ac=Ac, Bc=Bc, Q=Q, R=R, P=P, x_min=x_min, x_max=-x_min,
+                u_min=-8.0, u_max=8.0, xi0=np.array([2.0, 0.0, 0.0, 0.0]), xi_ref=xr)

@@ -1,0 +1,300 @@
+"""Generate the golden fixtures in tests/golden/ -- an INDEPENDENT numpy/scipy restatement of the
+reference hot path (it does not use oracle/ or libmpcqp).
+
+Reference (Fleming-Sung/mpc-limX-control @ 2025-04-04) restated here:
+  QPSolver::discretizeSystem  src/QPSolver.cpp:21-29  -> scipy.linalg.expm of [[Ac,Bc],[0,0]] Ts
+  QPSolver::buildQPParams     src/QPSolver.cpp:31-81  -> literal dense B_aug' Q_bar B_aug
+  linear_mpc_example Bd       src/linear_mpc_example.cpp:35-46
+  qp_test harness             src/qpSolver_test.cpp:6-90 (500-tick loop, xi-from-zero quirk)
+  mpcQP::buildSystemModel     include/mpcQP.h:139-181 (literal 13x3 model)
+The reference cannot be built here (Eigen/qpOASES absent) and ships no test vectors, so these
+fixtures pin the restatements to each other and to the SURVEY.md section 8c known-answer
+values, not to the reference binary ("parity unpinned" w.r.t. the binary).
+
+QP optima are certified independently of the Goldfarb-Idnani solvers under test: SLSQP start,
+then a primal-dual active-set polish that solves the KKT system exactly and checks
+stationarity, primal feasibility, dual feasibility and complementarity.
+
+Run:  python tests/golden/make_golden.py     (writes *.npz next to this file, ~1 min)
+"""
+from __future__ import annotations
+
+import math
+import os
+import sys
+
+import numpy as np
+import scipy.linalg as sl
+from scipy.optimize import linprog, minimize
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "mpc-limx-control_amd"))
+from mpcqp.model import model_params  # noqa: E402  (constants only)
+from mpcqp.workload import make_batch, qp_harness_inputs  # noqa: E402  (inputs only)
+
+INF = 1e20
+
+
+# ----------------------------------------------------------------- reference restatement
+def discretize(Ac, Bc, Ts):
+    nx, nu = Bc.shape
+    M = np.zeros((nx + nu, nx + nu))
+    M[:nx, :nx] = Ac
+    M[:nx, nx:] = Bc
+    E = sl.expm(M * Ts)
+    return E[:nx, :nx], E[:nx, nx:]
+
+
+def discretize_quadrature(Ac, Bc, Ts, steps=100):
+    Ad = sl.expm(Ac * Ts)
+    Bd = np.zeros_like(Bc)
+    I = np.eye(Ac.shape[0])
+    for i in range(steps):
+        tau = i * Ts / steps
+        Bd += Ad @ np.linalg.inv(I - Ac * tau / steps) @ Bc * (Ts / steps)
+    return Ad, Bd
+
+
+def build_qp(Ad, Bd, Q, R, P, x_min, x_max, u_min, u_max, xi0, xi_ref, N):
+    nx, nu = Bd.shape
+    Aaug = np.zeros((nx * (N + 1), nx))
+    Aaug[:nx] = np.eye(nx)
+    for i in range(1, N + 1):
+        Aaug[i * nx:(i + 1) * nx] = Ad @ Aaug[(i - 1) * nx:i * nx]
+    Baug = np.zeros((nx * (N + 1), nu * N))
+    for i in range(1, N + 1):
+        for j in range(i):
+            Baug[i * nx:(i + 1) * nx, j * nu:(j + 1) * nu] = np.linalg.matrix_power(Ad, i - j - 1) @ Bd
+    Qb = np.zeros((nx * (N + 1),) * 2)
+    Rb = np.zeros((nu * N,) * 2)
+    for i in range(N):
+        Qb[i * nx:(i + 1) * nx, i * nx:(i + 1) * nx] = Q
+        Rb[i * nu:(i + 1) * nu, i * nu:(i + 1) * nu] = R
+    Qb[N * nx:, N * nx:] = P
+    H = 2 * (Baug.T @ Qb @ Baug + Rb)
+    f = 2 * Baug.T @ Qb @ (Aaug @ xi0 - np.asarray(xi_ref).reshape(-1, order="F"))
+    out = dict(H=H, f=f, A_eq=Baug[nx:], b_eq=Aaug[nx:] @ xi0,
+               lb=np.full(nu * N, u_min), ub=np.full(nu * N, u_max))
+    Ain = np.zeros((2 * nx * N, nu * N))
+    lbA = np.full(2 * nx * N, -INF)
+    ubA = np.full(2 * nx * N, INF)
+    if x_min is not None:
+        for i in range(N):
+            Ain[2 * i * nx:(2 * i + 1) * nx] = Baug[(i + 1) * nx:(i + 2) * nx]
+            fr = np.linalg.matrix_power(Ad, i + 1) @ xi0
+            lbA[2 * i * nx:(2 * i + 1) * nx] = x_min - fr
+            ubA[2 * i * nx:(2 * i + 1) * nx] = x_max - fr
+    out.update(A_ineq=Ain, lbA=lbA, ubA=ubA)
+    return out
+
+
+def model_literal(dx, dy, dz, m):
+    Ac = np.zeros((13, 13))
+    Bc = np.zeros((13, 3))
+    Ac[0, 7], Ac[0, 8] = dz, dy
+    Ac[1, 6], Ac[1, 8] = dz, dx
+    Ac[2, 6], Ac[2, 7] = dy, dx
+    Ac[3, 9] = Ac[4, 10] = Ac[5, 11] = 1.0
+    Ac[11, 12] = -1.0
+    Bc[9, 0] = Bc[10, 1] = Bc[11, 2] = -m
+    return Ac, Bc
+
+
+def model_srbm(lin, m, Ib):
+    yaw = lin[0]
+    c, s = math.cos(yaw), math.sin(yaw)
+    Rz = np.array([[c, -s, 0], [s, c, 0], [0, 0, 1.0]])
+    Ac = np.zeros((13, 13))
+    Ac[0:3, 6:9] = Rz.T
+    Ac[3:6, 9:12] = np.eye(3)
+    Ac[11, 12] = 1.0
+    Iwi = Rz @ np.linalg.inv(Ib) @ Rz.T
+    Bc = np.zeros((13, 6))
+    for ft in range(2):
+        r = lin[1 + 3 * ft:4 + 3 * ft]
+        X = np.array([[0, -r[2], r[1]], [r[2], 0, -r[0]], [-r[1], r[0], 0]])
+        Bc[6:9, 3 * ft:3 * ft + 3] = Iwi @ X
+        Bc[9:12, 3 * ft:3 * ft + 3] = np.eye(3) / m
+    return Ac, Bc
+
+
+def srbm_bounds(p, contact):
+    nu, N = p["nu"], p["N"]
+    lb = np.zeros(nu * N)
+    ub = np.zeros(nu * N)
+    for k in range(N):
+        if p["model"] == 1:
+            lb[k * nu:(k + 1) * nu], ub[k * nu:(k + 1) * nu] = p["u_min"], p["u_max"]
+            continue
+        for s in range(2):
+            b = k * nu + 3 * s
+            if (int(contact) >> (2 * k + s)) & 1:
+                lb[b:b + 2], ub[b:b + 2] = -p["fxy_max"], p["fxy_max"]
+                lb[b + 2], ub[b + 2] = p["fz_min"], p["fz_max"]
+    return lb, ub
+
+
+def friction_rows(p, contact):
+    nu, N = p["nu"], p["N"]
+    G = []
+    for k in range(N):
+        for s in range(2):
+            if not (int(contact) >> (2 * k + s)) & 1:
+                continue
+            base = k * nu + 3 * s
+            for t in range(4):
+                g = np.zeros(nu * N)
+                g[base + 2] = p["mu"]
+                g[base + (t >> 1)] = 1.0 if (t & 1) else -1.0
+                G.append(g)
+    return np.array(G).reshape(-1, nu * N)
+
+
+# ----------------------------------------------------------------- independent QP certificate
+def qp_certified(H, f, lb, ub, A=None, lbA=None, ubA=None, G_extra=None):
+    """min 1/2 x'Hx + f'x with bounds / rows; returns (x, cost, kkt) or raises."""
+    n = H.shape[0]
+    fixed = lb == ub
+    G, h = [], []
+    for i in range(n):
+        if fixed[i]:
+            continue
+        if lb[i] > -INF:
+            e = np.zeros(n); e[i] = 1.0; G.append(e); h.append(lb[i])
+        if ub[i] < INF:
+            e = np.zeros(n); e[i] = -1.0; G.append(e); h.append(-ub[i])
+    if A is not None:
+        for r in range(A.shape[0]):
+            if lbA[r] > -INF:
+                G.append(A[r]); h.append(lbA[r])
+            if ubA[r] < INF:
+                G.append(-A[r]); h.append(-ubA[r])
+    if G_extra is not None:
+        for g in G_extra:
+            G.append(g); h.append(0.0)
+    G = np.array(G).reshape(-1, n)
+    h = np.array(h)
+    E = np.eye(n)[fixed]
+    e = lb[fixed]
+    # SLSQP start
+    x0 = np.where(fixed, lb, np.clip(np.zeros(n), np.maximum(lb, -1e3), np.minimum(ub, 1e3)))
+    cons = [dict(type="ineq", fun=lambda x: G @ x - h, jac=lambda x: G)]
+    if E.shape[0]:
+        cons.append(dict(type="eq", fun=lambda x: E @ x - e, jac=lambda x: E))
+    res = minimize(lambda x: 0.5 * x @ H @ x + f @ x, x0, jac=lambda x: H @ x + f,
+                   constraints=cons, method="SLSQP", options=dict(maxiter=2000, ftol=1e-14))
+    x = res.x
+    # primal-dual active-set polish with exact KKT solves
+    scale = 1.0 + np.abs(h)
+    act = set(np.nonzero(G @ x - h <= 1e-6 * scale)[0].tolist())
+    for _ in range(200):
+        a = sorted(act)
+        Ga = G[a]
+        K = np.block([[H, -Ga.T, -E.T], [Ga, np.zeros((len(a), len(a) + E.shape[0]))],
+                      [E, np.zeros((E.shape[0], len(a) + E.shape[0]))]])
+        rhs = np.concatenate([-f, h[a], e])
+        sol = np.linalg.lstsq(K, rhs, rcond=None)[0]
+        x = sol[:n]
+        lam = sol[n:n + len(a)]
+        viol = G @ x - h
+        bad_l = np.argmin(lam) if len(a) else None
+        if len(a) and lam[bad_l] < -1e-9 * (1 + np.abs(lam).max()):
+            act.discard(a[bad_l])
+            continue
+        worst = np.argmin(viol / scale)
+        if viol[worst] < -1e-10 * scale[worst]:
+            act.add(int(worst))
+            continue
+        nu_e = sol[n + len(a):]
+        stat = H @ x + f - Ga.T @ lam - E.T @ nu_e
+        kkt = dict(stationarity=float(np.abs(stat).max()),
+                   primal=float(max(0.0, -(viol / scale).min()) if len(h) else 0.0),
+                   dual=float(max(0.0, -lam.min()) if len(a) else 0.0),
+                   compl=float(np.abs(lam * viol[a]).max() if len(a) else 0.0))
+        assert kkt["stationarity"] < 1e-8 * (1 + np.abs(f).max()), kkt
+        return x, float(0.5 * x @ H @ x + f @ x), kkt
+    raise RuntimeError("active-set polish did not converge")
+
+
+def feasible_lp(A_eq, b_eq, A_ub, b_ub, bounds):
+    r = linprog(np.zeros(A_eq.shape[1]), A_ub=A_ub, b_ub=b_ub, A_eq=A_eq, b_eq=b_eq,
+                bounds=bounds, method="highs")
+    return r.status == 0
+
+
+# ----------------------------------------------------------------- fixtures
+def gen_a0():
+    h = qp_harness_inputs(0)
+    Ad, Bd = discretize(h["Ac"], h["Bc"], h["Ts"])
+    N = h["N"]
+    out = dict(Ac=h["Ac"], Bc=h["Bc"], Ts=h["Ts"], N=N, Q=h["Q"], R=h["R"], P=h["P"],
+               x_min=h["x_min"], x_max=h["x_max"], u_min=h["u_min"], u_max=h["u_max"], Ad=Ad,
+               Bd=Bd)
+    Ad_q, Bd_q = discretize_quadrature(h["Ac"], h["Bc"], h["Ts"])
+    out.update(Ad_quad=Ad_q, Bd_quad=Bd_q)
+    # qp_test closed loop with the corrected QP: the first QP sees xi = (2,0,0,0), the plant
+    # state (QPSolver::xi) starts at zero, later QPs see getState().  src/qpSolver_test.cpp:29-75
+    plant = np.zeros(4)
+    xi = h["xi0"].copy()
+    traj, useq = [], []
+    K = 500
+    for k in range(K):
+        hk = qp_harness_inputs(k)
+        q = build_qp(Ad, Bd, h["Q"], h["R"], h["P"], h["x_min"], h["x_max"], -8, 8, xi,
+                     hk["xi_ref"], N)
+        x, cost, kkt = qp_certified(q["H"], q["f"], q["lb"], q["ub"], q["A_ineq"], q["lbA"],
+                                    q["ubA"])
+        if k in (0, 1, 250):
+            for key, v in q.items():
+                out[f"k{k}_{key}"] = v
+            out[f"k{k}_xi0"] = xi.copy()
+            out[f"k{k}_xi_ref"] = hk["xi_ref"]
+            out[f"k{k}_U"] = x
+            out[f"k{k}_cost"] = cost
+            # the reference's stacked problem (A_eq rows as equalities) is infeasible
+            rows = [r for r in range(q["A_ineq"].shape[0]) if q["lbA"][r] > -INF]
+            Aub = np.vstack([q["A_ineq"][rows], -q["A_ineq"][rows]])
+            bub = np.concatenate([q["ubA"][rows], -q["lbA"][rows]])
+            out[f"k{k}_faithful_feasible"] = feasible_lp(q["A_eq"], q["b_eq"], Aub, bub,
+                                                         [(-8, 8)] * (2 * N))
+        u = x[:2]
+        plant = Ad @ plant + Bd @ u
+        xi = plant.copy()
+        traj.append(xi.copy())
+        useq.append(u.copy())
+    out["loop_states"] = np.array(traj)
+    out["loop_u"] = np.array(useq)
+    np.savez_compressed(os.path.join(HERE, "a0_harness.npz"), **out)
+
+
+def gen_srbm(config, B, keepH, seed, fname):
+    p = model_params(config)
+    b = make_batch(p, B, seed=seed, candidates=4)
+    nV = p["nu"] * p["N"]
+    Ads, Bds, Hs, fs, Us, costs, lbs, ubs = [], [], [], [], [], [], [], []
+    for i in range(B):
+        if p["model"] == 1:
+            Ac, Bc = model_literal(*b["lin"][i, :3], p["mass"])
+        else:
+            Ac, Bc = model_srbm(b["lin"][i], p["mass"], p["Ib"])
+        Ad, Bd = discretize(Ac, Bc, p["Ts"])
+        q = build_qp(Ad, Bd, p["Q"], p["R"], p["P"], None, None, 0, 0, b["x0"][i],
+                     b["xref"][i].T, p["N"])
+        lb, ub = srbm_bounds(p, b["contact"][i])
+        Gx = friction_rows(p, b["contact"][i]) if (p["friction"] and p["model"] == 0) else None
+        x, cost, kkt = qp_certified(q["H"], q["f"], lb, ub, G_extra=Gx)
+        Ads.append(Ad); Bds.append(Bd); Hs.append(q["H"]); fs.append(q["f"]); Us.append(x)
+        costs.append(cost); lbs.append(lb); ubs.append(ub)
+    np.savez_compressed(os.path.join(HERE, fname), config=config, seed=seed, x0=b["x0"],
+                        xref=b["xref"], lin=b["lin"], contact=b["contact"], Ad=np.array(Ads),
+                        Bd=np.array(Bds), H=np.array(Hs[:keepH]), f=np.array(fs),
+                        U=np.array(Us), cost=np.array(costs), lb=np.array(lbs),
+                        ub=np.array(ubs))
+
+
+if __name__ == "__main__":
+    gen_a0()
+    gen_srbm("B", 24, 6, 7, "srbm_B.npz")
+    gen_srbm("C", 8, 3, 11, "srbm_C.npz")
+    gen_srbm("L", 6, 3, 13, "literal_L.npz")
+    print("golden fixtures written to", HERE)

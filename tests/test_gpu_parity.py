@@ -1,0 +1,235 @@
+"""GPU parity: libmpcqp.so (HIP, gfx950) through its C ABI vs the golden fixtures and the CPU
+oracle on identical seeded inputs.  Floating point throughout (fp64, the reference's Eigen
+MatrixXd arithmetic); tolerances are stated per quantity:
+  Ad, Bd                    <= 1e-13 norm-wise relative
+  H, f, constraint arrays   <= 1e-12 norm-wise relative
+  QP optimum U              ||dU||_inf <= 1e-8 * max(1, ||U||_inf)      
+  cost                      <= 1e-9 relative
+"""
+import numpy as np
+import pytest
+
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+
+TOL_DISC = 1e-13
+TOL_COND = 1e-12
+TOL_U = 1e-8
+
+
+def u_close(U, U0):
+    return np.abs(np.asarray(U) - U0).max() <= TOL_U * max(1.0, np.abs(U0).max())
+
+
+# ------------------------------------------------------------- single-instance reference API
+def test_discretize_reference_plant(gpu, golden):
+    from mpcqp.qpsolver import discretize
+    g = golden("a0_harness.npz")
+    Ad, Bd = discretize(g["Ac"], g["Bc"], float(g["Ts"]))
+    assert rel_err(Ad, g["Ad"]) <= TOL_DISC and rel_err(Bd, g["Bd"]) <= TOL_DISC
+    assert Bd[0, 0] == pytest.approx(2.4991668749583e-4, rel=1e-12)  # SURVEY 8c KAT
+
+
+@pytest.mark.parametrize("scale", [1e-3, 0.1, 0.5, 1.5, 8.0, 60.0])
+def test_discretize_all_pade_degrees(gpu, orc, scale):
+    from mpcqp.qpsolver import discretize
+    rng = np.random.default_rng(int(scale * 1000))
+    for nx, nu in ((4, 2), (13, 6), (24, 6)):
+        Ac = rng.normal(size=(nx, nx))
+        Bc = rng.normal(size=(nx, nu))
+        M = np.zeros((nx + nu, nx + nu))
+        M[:nx, :nx], M[:nx, nx:] = Ac, Bc
+        Ts = scale / np.abs(M).sum(0).max()
+        Ad, Bd = discretize(Ac, Bc, Ts)
+        Ad0, Bd0 = orc.discretize(Ac, Bc, Ts)
+        assert rel_err(Ad, Ad0) <= 1e-12 and rel_err(Bd, Bd0) <= 1e-12, (nx, nu)
+
+
+@pytest.mark.parametrize("k", [0, 1, 250])
+def test_build_qp_reference_layout(gpu, golden, k):
+    from mpcqp.qpsolver import build_qp
+    g = golden("a0_harness.npz")
+    o = build_qp(g["Ad"], g["Bd"], g["Q"], g["R"], g["P"], g["x_min"], g["x_max"], -8, 8,
+                 g[f"k{k}_xi0"], g[f"k{k}_xi_ref"], int(g["N"]))
+    for key in ("H", "f", "A_eq", "b_eq", "lb", "ub", "A_ineq"):
+        assert rel_err(o[key], g[f"k{k}_{key}"]) <= TOL_COND, key
+    for key in ("lbA", "ubA"):
+        a, b = o[key], g[f"k{k}_{key}"]
+        fin = np.abs(b) < 1e19
+        assert rel_err(a[fin], b[fin]) <= TOL_COND
+        np.testing.assert_array_equal(a[~fin], b[~fin])
+
+
+@pytest.mark.parametrize("k", [0, 1, 250])
+def test_solve_dense_corrected_and_faithful(gpu, golden, orc, k):
+    from mpcqp.qpsolver import solve_dense
+    g = golden("a0_harness.npz")
+    H, f, lb, ub = g[f"k{k}_H"], g[f"k{k}_f"], g[f"k{k}_lb"], g[f"k{k}_ub"]
+    A, lbA, ubA = g[f"k{k}_A_ineq"], g[f"k{k}_lbA"], g[f"k{k}_ubA"]
+    st, x, cost, it, y = solve_dense(H, f, A, lb, ub, lbA, ubA, want_y=True)
+    assert st == 0
+    assert u_close(x, g[f"k{k}_U"])
+    assert cost == pytest.approx(float(g[f"k{k}_cost"]), rel=1e-9)
+    st0, x0, c0, it0, lb0, lr0 = orc.solve_qp(H, f, lb, ub, A, lbA, ubA)
+    assert it == it0
+    np.testing.assert_allclose(H @ x + f, y[:30] + A.T @ y[30:], atol=1e-9)
+    np.testing.assert_allclose(y[:30], lb0, atol=1e-8)
+    # the reference's stacked [A_eq; A_ineq] problem is infeasible: reported, not hidden
+    Af = np.vstack([g[f"k{k}_A_eq"], A])
+    bl = np.concatenate([g[f"k{k}_b_eq"], lbA])
+    bu = np.concatenate([g[f"k{k}_b_eq"], ubA])
+    st2, *_ = solve_dense(H, f, Af, lb, ub, bl, bu)
+    assert st2 == 2
+
+
+def test_qpsolver_class_closed_loop(gpu, golden):
+    """qp_test (src/qpSolver_test.cpp:26-90) through the reference-shaped QPSolver mirror."""
+    from mpcqp.qpsolver import QPSolver
+    import mpcqp
+    g = golden("a0_harness.npz")
+    h = mpcqp.qp_harness_inputs(0)
+    qp = QPSolver(h["Ts"], h["N"], h["Ac"], h["Bc"], h["Q"], h["R"], h["P"], h["x_min"],
+                  h["x_max"], h["u_min"], h["u_max"])
+    xi = h["xi0"].copy()
+    for k in range(100):
+        hk = mpcqp.qp_harness_inputs(k)
+        H, f, A_eq, b_eq, lb, ub, A_ineq, lbA, ubA = qp.buildQPParams(xi, hk["xi_ref"])
+        A_total = np.vstack([A_eq, A_ineq])
+        ok, U_opt = qp.solveQP(H, f, A_total, lb, ub, np.concatenate([b_eq, lbA]),
+                               np.concatenate([b_eq, ubA]))
+        assert ok and qp.corrected and qp.last_status == 0
+        qp.updateState(U_opt[:, 0])
+        xi = qp.getState()
+    np.testing.assert_allclose(xi, g["loop_states"][99], rtol=1e-7, atol=1e-9)
+
+
+# ------------------------------------------------------------------------- batched engine
+def run_batch(p, batch, want_hf=False):
+    from mpcqp.engine import BatchEngine
+    eng = BatchEngine(p)
+    d = eng.upload(batch)
+    out = {}
+    if want_hf:
+        H, f = eng.condense(d)
+        eng.solve_qp(d, H, f)
+        eng.sync()
+        out["H"] = H.cpu().numpy().transpose(0, 2, 1)  # stored column-major per instance
+        out["f"] = f.cpu().numpy()
+    else:
+        eng.solve(d)
+        eng.sync()
+    for k in ("U", "cost", "status", "iters"):
+        out[k] = d[k].cpu().numpy()
+    eng.close()
+    return out
+
+
+@pytest.mark.parametrize("fname", ["srbm_B.npz", "srbm_C.npz", "literal_L.npz"])
+def test_batch_vs_golden(gpu, golden, fname):
+    import mpcqp
+    g = golden(fname)
+    p = mpcqp.model_params(str(g["config"]))
+    batch = dict(x0=g["x0"], xref=g["xref"], lin=g["lin"], contact=g["contact"])
+    o = run_batch(p, batch, want_hf=True)
+    assert np.all(o["status"] == 0)
+    for i in range(g["H"].shape[0]):
+        assert rel_err(o["H"][i], g["H"][i]) <= TOL_COND
+    for i in range(g["f"].shape[0]):
+        assert rel_err(o["f"][i], g["f"][i]) <= TOL_COND
+        assert u_close(o["U"][i], g["U"][i]), i
+        assert o["cost"][i] == pytest.approx(float(g["cost"][i]), rel=1e-9, abs=1e-9)
+
+
+@pytest.mark.parametrize("config,B", [("B", 2048), ("C", 512), ("L", 512)])
+def test_batch_vs_oracle(gpu, orc, config, B):
+    import mpcqp
+    p = mpcqp.model_params(config)
+    batch = mpcqp.make_batch(p, B, seed=99)
+    o = run_batch(p, batch, want_hf=True)
+    ref = orc.srbm_batch(p, batch["x0"], batch["xref"], batch["lin"], batch["contact"],
+                         want_hf=True)
+    np.testing.assert_array_equal(o["status"], ref["status"])
+    assert np.all(o["status"] == 0)
+    for i in range(0, B, max(1, B // 64)):
+        assert rel_err(o["H"][i], ref["H"][i]) <= TOL_COND
+        assert rel_err(o["f"][i], ref["f"][i]) <= TOL_COND
+    bad = [i for i in range(B) if not u_close(o["U"][i], ref["U"][i])]
+    assert not bad, bad[:10]
+    np.testing.assert_allclose(o["cost"], ref["cost"], rtol=1e-9, atol=1e-9)
+    # same algorithm, same order: iteration counts agree except on rounding-level ties
+    assert np.mean(o["iters"] == ref["iters"]) >= 0.99
+
+
+def test_full_size_metric_batch_properties(gpu, orc):
+    """BASELINE metric config (13/6/10, batch 65536): size-independent properties --
+    every instance solved, KKT-consistent sample against the oracle, bitwise determinism
+    across two runs, and the min-cost key equals the host argmin of the returned costs."""
+    import mpcqp
+    from mpcqp.engine import BatchEngine, decode_key, encode_key
+    p = mpcqp.model_params("B")
+    B = 65536
+    batch = mpcqp.make_batch(p, B)
+    eng = BatchEngine(p)
+    d = eng.upload(batch)
+    eng.solve(d)
+    key = int(eng.select_min(d).item())
+    U1 = d["U"].cpu().numpy().copy()
+    c1 = d["cost"].cpu().numpy().copy()
+    st = d["status"].cpu().numpy()
+    eng.solve(d)
+    eng.sync()
+    U2 = d["U"].cpu().numpy()
+    eng.close()
+    assert np.all(st == 0)
+    np.testing.assert_array_equal(U1, U2)  # deterministic
+    host_key = min(encode_key(c, i) for i, c in enumerate(c1))
+    assert key == host_key
+    cbest, ibest = decode_key(key)
+    assert ibest == int(np.lexsort((np.arange(B), c1.astype(np.float32)))[0])
+    idx = np.random.default_rng(5).choice(B, 192, replace=False)
+    sub = {k: batch[k][idx] for k in batch}
+    ref = orc.srbm_batch(p, sub["x0"], sub["xref"], sub["lin"], sub["contact"])
+    for j, i in enumerate(idx):
+        assert u_close(U1[i], ref["U"][j]), i
+
+
+def test_edge_cases(gpu):
+    """empty batch, infeasible bounds, no free variable, non-PD Hessian, too many free vars"""
+    from mpcqp.qpsolver import solve_dense
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    # empty batch
+    p = mpcqp.model_params("B")
+    eng = BatchEngine(p)
+    d = eng.upload({k: v[:0] for k, v in mpcqp.make_batch(p, 4).items()})
+    eng.solve(d)
+    eng.sync()
+    eng.close()
+    H = np.diag([2.0, 4.0, 1.0])
+    f = np.array([1.0, -2.0, 0.5])
+    st, *_ = solve_dense(H, f, None, np.array([0.0, 1.0, 0.0]), np.array([1.0, 0.0, 1.0]))
+    assert st == 2  # lb > ub
+    st, x, cost, it, _ = solve_dense(H, f, None, np.array([0.5, 1.0, -1.0]),
+                                     np.array([0.5, 1.0, -1.0]))
+    assert st == 0 and np.allclose(x, [0.5, 1.0, -1.0])
+    assert cost == pytest.approx(0.5 * x @ H @ x + f @ x)
+    st, *_ = solve_dense(np.diag([1.0, -1.0, 1.0]), f, None, None, None)
+    assert st == 4  # not positive definite
+    # unbounded-below directions are impossible for PD H; a bounds-only QP hits the box
+    st, x, *_ = solve_dense(H, np.array([-100.0, 100.0, 0.0]), None, -np.ones(3), np.ones(3))
+    assert st == 0 and np.allclose(x, [1.0, -1.0, 0.0])
+    # equality row: x0 + x1 = 1
+    st, x, *_ = solve_dense(H, f, np.array([[1.0, 1.0, 0.0]]), None, None, np.array([1.0]),
+                            np.array([1.0]))
+    assert st == 0 and x[0] + x[1] == pytest.approx(1.0, abs=1e-12)
+    # more free variables than the batched context was sized for -> BAD_DIMS per instance
+    p2 = mpcqp.model_params("B")
+    p2["max_free"] = 12
+    batch = mpcqp.make_batch(p2, 8)
+    eng = BatchEngine(p2)
+    d = eng.upload(batch)
+    eng.solve(d)
+    eng.sync()
+    assert np.all(d["status"].cpu().numpy() == 1)
+    eng.close()
