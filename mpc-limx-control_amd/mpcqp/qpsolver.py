@@ -41,7 +41,8 @@ def discretize(Ac, Bc, Ts):
     nx, nu = Bc.shape
     Ad = np.zeros(nx * nx)
     Bd = np.zeros(nx * nu)
-    check("mpcqp_discretize", lib().mpcqp_discretize(nx, nu, float(Ts), _p(_f(Ac)), _p(_f(Bc)),
+    fAc, fBc = _f(Ac), _f(Bc)  # keep the buffers alive across the call
+    check("mpcqp_discretize", lib().mpcqp_discretize(nx, nu, float(Ts), _p(fAc), _p(fBc),
                                                      _p(Ad), _p(Bd)))
     return Ad.reshape(nx, nx, order="F"), Bd.reshape(nx, nu, order="F")
 
@@ -130,8 +131,9 @@ class QPSolver:
     def updateState(self, u):
         x = np.ascontiguousarray(self.xi, dtype=np.float64).copy()
         uu = np.ascontiguousarray(np.asarray(u, float).reshape(-1))
+        fAd, fBd = _f(self.Ad), _f(self.Bd)
         check("mpcqp_plant_step", lib().mpcqp_plant_step(
-            self.NX, self.NU, _p(_f(self.Ad)), _p(_f(self.Bd)), _p(x), _p(uu)))
+            self.NX, self.NU, _p(fAd), _p(fBd), _p(x), _p(uu)))
         self.xi = x
         if self.verbose:
             print(" ".join(f"{v:g}" for v in self.xi))
