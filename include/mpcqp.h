@@ -27,6 +27,10 @@
  * mpcqp_batch_solve               mpcQP::mpcQP ctor end to end (include/mpcQP.h:35-119),
  *                                 i.e. the intended MPC::computeSupportFootForce
  *                                 (include/MPCController.h:178-180), batched
+ * mpcqp_batch_discretize          mpcQP::buildSystemModel + QPSolver::discretizeSystem,
+ *                                 batched -> [Ad | Bd] per instance
+ * mpcqp_batch_condense_solve      QPSolver::buildQPParams + QPSolver::solveQP, batched, fused
+ *                                 (H never leaves the chip)
  * mpcqp_batch_select_min          (new) per-rank min-cost key for the multi-GPU selection
  */
 #ifndef MPCQP_H
@@ -129,11 +133,23 @@ int mpcqp_ctx_destroy(mpcqp_ctx *ctx);
 int mpcqp_set_stream(mpcqp_ctx *ctx, void *stream);
 int mpcqp_sync(mpcqp_ctx *ctx);
 
+/* 1 when the context runs the compile-time-dimension fused kernels (13/6/{10,20} SRBM,
+ * 13/3/{10,20} literal, diagonal Q and P), 0 when it runs the generic kernels */
+int mpcqp_ctx_fast_path(const mpcqp_ctx *ctx);
+
+/* stage 1: linearise + discretise.  AB [B][nx*(nx+nu)] = [Ad | Bd] column-major */
+int mpcqp_batch_discretize(mpcqp_ctx *ctx, int B, const double *lin, double *AB);
+/* stage 2: condense + solve from AB, fused (H stays on chip) */
+int mpcqp_batch_condense_solve(mpcqp_ctx *ctx, int B, const double *AB, const double *x0,
+                               const double *xref, const uint64_t *contact, double *U,
+                               double *cost, int *status, int *iters);
+/* full H [B][nV][nV] (column-major) and f [B][nV] of the whole QP (parity / inspection) */
 int mpcqp_batch_condense(mpcqp_ctx *ctx, int B, const double *x0, const double *xref,
                          const double *lin, double *H, double *f);
 int mpcqp_batch_solve_qp(mpcqp_ctx *ctx, int B, const double *H, const double *f,
                          const uint64_t *contact, double *U, double *cost, int *status,
                          int *iters);
+/* stage 1 + stage 2 */
 int mpcqp_batch_solve(mpcqp_ctx *ctx, int B, const double *x0, const double *xref,
                       const double *lin, const uint64_t *contact, double *U, double *cost,
                       int *status, int *iters);
@@ -143,10 +159,11 @@ int mpcqp_batch_solve(mpcqp_ctx *ctx, int B, const double *x0, const double *xre
 int mpcqp_batch_select_min(mpcqp_ctx *ctx, int B, const double *cost, const int *status,
                            int64_t index_base, int64_t *key);
 
-/* last kernel duration of the dominant kernel measured with HIP events on the ctx stream
- * (ms; -1 if none) -- used by bench.py for the roofline figure */
+/* duration of the last stage-1 (which = 0: discretize / generic condense) or stage-2
+ * (which = 1: condense_solve / generic solve) kernel, HIP events on the ctx stream (ms; -1 if
+ * none recorded).  Timing is off until enabled. */
 int mpcqp_enable_timing(mpcqp_ctx *ctx, int on);
-double mpcqp_last_kernel_ms(mpcqp_ctx *ctx, int which /* 0 condense, 1 solve, 2 fused */);
+double mpcqp_last_kernel_ms(mpcqp_ctx *ctx, int which);
 
 const char *mpcqp_status_string(int status);
 int mpcqp_device_count(void);

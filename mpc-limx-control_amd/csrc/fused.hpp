@@ -1,0 +1,223 @@
+// fused.hpp -- the batched hot path with compile-time dimensions (gfx950).
+//
+//   k_discretize<NX,NU,MODEL>          linearise (SRBM / reference-literal) and exp(M Ts)
+//                                       -> [Ad | Bd] (NX x (NX+NU), 2 KB per QP at 13/6)
+//   k_condense_solve<NX,NU,N,...>      Phi_k = Ad^k Bd, free-variable Hessian block H_FF,
+//                                       gradient f_F, Goldfarb-Idnani solve -- H never
+//                                       leaves LDS; only U, cost, status, iters are stored.
+//
+// Reference: mpcQP::buildSystemModel include/mpcQP.h:121-182, QPSolver::discretizeSystem
+// src/QPSolver.cpp:21-29, QPSolver::buildQPParams :31-81, QPSolver::solveQP :83-106.
+//
+// Only the free block of H is formed: in the SRBM model the swing foot's inputs are fixed at
+// zero by the contact schedule (lb == ub == 0), so they drop out of the QP exactly (their
+// H_FB x_B and f terms vanish); the reference would carry them as active bounds.
+//   H(i,j) = 2 [ sum_{m > max(k_i,k_j)} Phi_{m-1-k_i}[:,c_i]' W_m Phi_{m-1-k_j}[:,c_j]
+//              + R(c_i,c_j) [k_i == k_j] ],   W_m = Q (m < N), P (m = N)  (diagonal)
+//   f(i)   = 2 sum_{m > k_i} Phi_{m-1-k_i}[:,c_i]' W_m (Ad^m x0 - xref_m)
+#pragma once
+#include "condense.hpp"
+#include "gi_solver.hpp"
+
+namespace mpcqp {
+
+struct FastArgs {
+    int B;
+    // model
+    double Ts, mass;
+    double Ibinv[9];
+    const double *qd, *pd;                    // diagonal of Q and P (device, nx each)
+    const double *rmat;                       // R (nu x nu, column-major, device)
+    // bounds / constraints
+    double fz_min, fz_max, fxy_max, u_min, u_max, mu;
+    int max_iter;
+    int max_free;                             // model's free-variable bound (<= NFMAX)
+    // per-instance data
+    const double *lin, *x0, *xref;
+    const uint64_t *contact;
+    double *AB;                               // [B][NX*NS]
+    double *U, *cost;
+    int *status, *iters;
+};
+
+template <int NX, int NU>
+__host__ __device__ constexpr int disc_lds_doubles() {
+    return 9 * NX * (NX + NU);
+}
+
+// ------------------------------------------------------------------ k_discretize
+template <int NX, int NU, int MODEL>
+__device__ inline void fast_discretize(const FastArgs &a, double *smem) {
+    constexpr int NS = NX + NU;
+    const int b = blockIdx.x;
+    ModelConst mc;
+    mc.nx = NX; mc.nu = NU; mc.N = 1; mc.nV = NU; mc.ns = NS;
+    mc.model = MODEL; mc.Ts = a.Ts; mc.mass = a.mass;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) mc.Ibinv[i] = a.Ibinv[i];
+    mc.Q = mc.R = mc.P = nullptr;
+    double lin[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) lin[i] = a.lin[(size_t)b * 8 + i];
+    double *T = smem, *ws = smem + NX * NS, *E = smem + 8 * NX * NS;
+    wave_build_model(mc, lin, nullptr, nullptr, T);
+    wave_expm(NX, NS, T, ws, E);
+    double *out = a.AB + (size_t)b * NX * NS;
+    for (int e = lane(); e < NX * NS; e += kWave) out[e] = E[e];
+}
+
+// ------------------------------------------------------------------ k_condense_solve
+template <int NX, int NU, int N, bool FRIC, int NFMAX>
+struct CSLayout {
+    static constexpr int NS = NX + NU, NV = NU * N, LD = NFMAX | 1;
+    static constexpr int NFRIC = FRIC ? 4 * N * 2 : 0;
+    static constexpr int MT = 2 * NFMAX + NFRIC;
+    // doubles
+    static constexpr int oR = 0;
+    static constexpr int oG = oR + NFMAX * LD;
+    static constexpr int oXS = oG + NFMAX;
+    static constexpr int oXF = oXS + NFMAX;           // xfull (fixed values)
+    static constexpr int oYS = oXF + NV;              // (unused ys / rowfix slot)
+    static constexpr int oU = oYS + 2;                // union base
+    // union member 1: condensing
+    static constexpr int uAB = 0;
+    static constexpr int uPhi = uAB + NX * NS;
+    static constexpr int uXf = uPhi + NX * NV;
+    static constexpr int uQe = uXf + NX * (N + 1);
+    static constexpr int uCond = uQe + NX * (N + 1);
+    // union member 2: J
+    static constexpr int uJ = NFMAX * LD;
+    static constexpr int uSize = uCond > uJ ? uCond : uJ;
+    static constexpr int nDoubles = oU + uSize;
+    // ints / bytes after the doubles
+    static constexpr size_t bytes = sizeof(double) * nDoubles + sizeof(int) * (NFMAX + NV) +
+                                    ((MT + 15) & ~15);
+    static constexpr size_t lds_bytes = (bytes + 15) & ~(size_t)15;
+};
+
+template <int NX, int NU, int N, int MODEL, bool FRIC, int NFMAX>
+__device__ inline void fast_condense_solve(const FastArgs &a, unsigned char *smem) {
+    using Lay = CSLayout<NX, NU, N, FRIC, NFMAX>;
+    constexpr int NS = Lay::NS, NV = Lay::NV, LD = Lay::LD;
+    const int b = blockIdx.x, ln = lane();
+    double *D = reinterpret_cast<double *>(smem);
+    double *Un = D + Lay::oU;
+    double *AB = Un + Lay::uAB, *Phi = Un + Lay::uPhi, *xf = Un + Lay::uXf, *Qe = Un + Lay::uQe;
+
+    // ---- problem description for the solver stages (bounds from the contact schedule)
+    SolveProblem P;
+    P.nV = NV;
+    P.H = nullptr; P.f = nullptr; P.lb = nullptr; P.ub = nullptr;
+    P.gen_bounds = 1;
+    P.model = MODEL; P.nu = NU; P.N = N; P.nfeet = 2;
+    P.fz_min = a.fz_min; P.fz_max = a.fz_max; P.fxy_max = a.fxy_max;
+    P.u_min = a.u_min; P.u_max = a.u_max;
+    P.contact = (MODEL == 0) ? a.contact[b] : 0ull;
+    P.friction = FRIC ? 1 : 0;
+    P.mu = a.mu;
+    P.mA = 0; P.A = nullptr; P.a_colmajor = 0; P.lbA = nullptr; P.ubA = nullptr;
+    P.max_iter = a.max_iter;
+    GiCtx C;
+    C.P = &P;
+    C.nfmax = NFMAX;
+    C.L.ld = LD;
+    C.L.R = D + Lay::oR;
+    C.L.g = D + Lay::oG;
+    C.L.xs = D + Lay::oXS;
+    C.L.xfull = D + Lay::oXF;
+    C.L.rowfix = D + Lay::oYS;
+    C.L.ys = D + Lay::oYS;
+    C.L.J = Un;
+    int *ip = reinterpret_cast<int *>(D + Lay::nDoubles);
+    C.L.fid = ip;
+    C.L.pos = ip + NFMAX;
+    C.L.st = reinterpret_cast<unsigned char *>(ip + NFMAX + NV);
+
+    // ---- inputs
+    const double *ABg = a.AB + (size_t)b * NX * NS;
+    for (int e = ln; e < NX * NS; e += kWave) AB[e] = ABg[e];
+    if (ln < NX) xf[ln] = a.x0[(size_t)b * NX + ln];
+    gi_setup(C);  // free map + constraint states (independent of AB)
+    if (C.nf > a.max_free) C.status = ST_BAD_DIMS;
+    wave_sync();
+    const double *Ad = AB, *Bd = AB + NX * NX;
+
+    // ---- Phi_m = Ad Phi_{m-1} (Phi_0 = Bd) and free response xf_m = Ad xf_{m-1}
+    for (int e = ln; e < NX * NU; e += kWave) Phi[e] = Bd[e];
+    wave_sync();
+    for (int m = 1; m <= N; ++m) {
+        constexpr int nPhi = NX * NU;
+        const int tot = (m < N) ? nPhi + NX : NX;
+        for (int e = ln; e < tot; e += kWave) {
+            const bool isx = (m == N) || e >= nPhi;
+            const int i = isx ? (m < N ? e - nPhi : e) : e % NX;
+            const double *src = isx ? xf + (m - 1) * NX : Phi + (m - 1) * nPhi + (e / NX) * NX;
+            double s = 0.0;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) s += Ad[l * NX + i] * src[l];
+            if (isx) xf[m * NX + i] = s;
+            else Phi[m * nPhi + e] = s;
+        }
+        wave_sync();
+    }
+    // ---- weighted tracking errors Qe_m = W_m (xf_m - xref_m), m = 1..N
+    const double *xr = a.xref + (size_t)b * NX * (N + 1);
+    for (int e = ln; e < NX * N; e += kWave) {
+        const int i = e % NX, m = 1 + e / NX;
+        const double w = (m < N) ? a.qd[i] : a.pd[i];
+        Qe[m * NX + i] = w * (xf[m * NX + i] - xr[m * NX + i]);
+    }
+    wave_sync();
+
+    const int nf = C.nf;
+    if (C.status == ST_OK && nf > 0) {
+        // ---- H_FF lower triangle, (p >= q) packed index e
+        const int E = nf * (nf + 1) / 2;
+        for (int e = ln; e < E; e += kWave) {
+            int p = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+            while (p * (p + 1) / 2 > e) --p;
+            while ((p + 1) * (p + 2) / 2 <= e) ++p;
+            const int q = e - p * (p + 1) / 2;
+            const int vi = C.L.fid[p], vj = C.L.fid[q];
+            const int ki = vi / NU, ci = vi % NU, kj = vj / NU, cj = vj % NU;
+            const int kk = ki > kj ? ki : kj;
+            double s = 0.0;
+            for (int m = kk + 1; m <= N; ++m) {
+                const double *pa = Phi + ((m - 1 - ki) * NU + ci) * NX;
+                const double *pb = Phi + ((m - 1 - kj) * NU + cj) * NX;
+                const double *w = (m < N) ? a.qd : a.pd;  // wave-uniform: scalar loads
+                double t = 0.0;
+#pragma unroll
+                for (int l = 0; l < NX; ++l) t += pa[l] * w[l] * pb[l];
+                s += t;
+            }
+            if (ki == kj) s += a.rmat[cj * NU + ci];
+            C.L.R[q * LD + p] = 2.0 * s;
+        }
+        // ---- gradient of the free variables (fixed ones sit at 0 in this model)
+        for (int p = ln; p < nf; p += kWave) {
+            const int vi = C.L.fid[p], ki = vi / NU, ci = vi % NU;
+            double s = 0.0;
+            for (int m = ki + 1; m <= N; ++m) {
+                const double *pa = Phi + ((m - 1 - ki) * NU + ci) * NX;
+                double t = 0.0;
+#pragma unroll
+                for (int l = 0; l < NX; ++l) t += pa[l] * Qe[m * NX + l];
+                s += t;
+            }
+            C.L.g[p] = 2.0 * s;
+        }
+    }
+    C.c0 = 0.0;
+    wave_sync();
+    gi_run(C);
+    SolveOut O;
+    O.x = a.U + (size_t)b * NV;
+    O.cost = a.cost + b;
+    O.status = a.status + b;
+    O.iters = a.iters + b;
+    O.y = nullptr;
+    gi_write(C, O);
+}
+
+}  // namespace mpcqp

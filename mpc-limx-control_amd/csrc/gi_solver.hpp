@@ -12,6 +12,12 @@
 // free for ds_read_b64.  x is mirrored in LDS (xs) for the constraint sweeps.
 //   constraint ids: [0,nf) lower bounds, [nf,2nf) upper bounds,
 //                   [2nf, 2nf+4*N*nfeet) friction rows (k, s, t), then dense rows (r, side).
+//
+// Stages (so the fused condense+solve kernel can build H_FF in LDS itself):
+//   gi_setup      fixed variables, free index map, constraint states
+//   gi_gather     H_FF, g = f_F + H_FB x_B from global memory (stand-alone solve)
+//   gi_run        Cholesky, J = L^-T, unconstrained minimum, dual active-set loop
+//   gi_write      x, cost, status, iterations, optional multipliers
 #pragma once
 #include "wave_ops.hpp"
 
@@ -71,7 +77,7 @@ __host__ __device__ inline size_t gi_lds_bytes(int nfmax, int nV, int mA, int nf
 struct GiLds {
     double *J, *R, *g, *xs, *xfull, *rowfix, *ys;
     int *fid, *pos;
-    unsigned char *st;  // 0 absent, 1 inactive, 2 active, 3 pending equality, 4 infeasible
+    unsigned char *st;  // 0 absent, 1 inactive, 2 active, 3 equality, 4 infeasible
     int ld;
 };
 
@@ -92,6 +98,17 @@ __device__ inline GiLds gi_carve(unsigned char *base, int nfmax, int nV, int mA)
     L.st = reinterpret_cast<unsigned char *>(ip);
     return L;
 }
+
+struct GiCtx {
+    const SolveProblem *P;
+    GiLds L;
+    int nfmax, nf, nfric, mt;
+    int status;
+    double c0;     // objective contribution of the fixed variables
+    // results of gi_run
+    double x, u, fval;
+    int act, q, iters;
+};
 
 __device__ __forceinline__ double rowA(const SolveProblem &P, int r, int v) {
     return P.a_colmajor ? P.A[(size_t)v * P.mA + r] : P.A[(size_t)r * P.nV + v];
@@ -114,17 +131,98 @@ __device__ __forceinline__ void var_bounds(const SolveProblem &P, int v, double 
     hi = P.ub ? P.ub[v] : kInfty;
 }
 
-// Solve one instance.  LDS workspace carved from `smem` (gi_lds_bytes).
-__device__ inline void wave_gi_solve(const SolveProblem &P, const SolveOut &O,
-                                     unsigned char *smem, int nfmax) {
-    const int nV = P.nV, mA = P.mA;
-    const int ln = lane();
-    const int nfric = P.friction ? 4 * P.N * P.nfeet : 0;
-    GiLds L = gi_carve(smem, nfmax, nV, mA);
-    const int ld = L.ld;
-    int status = ST_OK;
+// ---------------------------------------------------------------- constraint accessors
+// b of the one-sided constraint id (normal' x_F >= b, fixed parts folded into b)
+__device__ inline double gi_cons_b(const GiCtx &C, int id) {
+    const SolveProblem &P = *C.P;
+    const GiLds &L = C.L;
+    const int nf = C.nf, nfric = C.nfric;
+    double lo, hi;
+    if (id < nf) { var_bounds(P, L.fid[id], lo, hi); return lo; }
+    if (id < 2 * nf) { var_bounds(P, L.fid[id - nf], lo, hi); return -hi; }
+    if (id < 2 * nf + nfric) {
+        const int r = id - 2 * nf, ks = r >> 2, t = r & 3;
+        const int k = ks / P.nfeet, sft = ks % P.nfeet;
+        const int vz = k * P.nu + 3 * sft + 2, vt = k * P.nu + 3 * sft + (t >> 1);
+        const double sg = (t & 1) ? 1.0 : -1.0;
+        double b = 0.0;
+        if (L.pos[vz] < 0) b -= P.mu * L.xfull[vz];
+        if (L.pos[vt] < 0) b -= sg * L.xfull[vt];
+        return b;
+    }
+    const int r = id - 2 * nf - nfric, row = r >> 1, side = r & 1;
+    return side ? (-P.ubA[row] + L.rowfix[row]) : (P.lbA[row] - L.rowfix[row]);
+}
 
-    // ---- fixed variables (lb == ub) and the free index map
+// slack n'x - b of constraint id evaluated by ONE lane (x read from the LDS mirror)
+__device__ inline double gi_cons_slack_lane(const GiCtx &C, int id) {
+    const SolveProblem &P = *C.P;
+    const GiLds &L = C.L;
+    const int nf = C.nf, nfric = C.nfric;
+    if (id < nf) return L.xs[id] - gi_cons_b(C, id);
+    if (id < 2 * nf) return -L.xs[id - nf] - gi_cons_b(C, id);
+    if (id < 2 * nf + nfric) {
+        const int r = id - 2 * nf, ks = r >> 2, t = r & 3;
+        const int k = ks / P.nfeet, sft = ks % P.nfeet;
+        const int vz = k * P.nu + 3 * sft + 2, vt = k * P.nu + 3 * sft + (t >> 1);
+        const double sg = (t & 1) ? 1.0 : -1.0;
+        const int pz = L.pos[vz], pt = L.pos[vt];
+        double s = 0.0;
+        if (pz >= 0) s += P.mu * L.xs[pz];
+        if (pt >= 0) s += sg * L.xs[pt];
+        return s - gi_cons_b(C, id);
+    }
+    const int r = id - 2 * nf - nfric, row = r >> 1, side = r & 1;
+    const double sg = side ? -1.0 : 1.0;
+    double s = 0.0;
+    for (int a = 0; a < nf; ++a) s += sg * rowA(P, row, L.fid[a]) * L.xs[a];
+    return s - gi_cons_b(C, id);
+}
+
+// d_j = (J' n_p)_j on lane j, and the slack n_p'x - b (uniform); x: lane i holds x_i
+__device__ inline void gi_cons_project(const GiCtx &C, int id, double x, double &dj, double &sp) {
+    const SolveProblem &P = *C.P;
+    const GiLds &L = C.L;
+    const int nf = C.nf, nfric = C.nfric, ld = L.ld, ln = lane();
+    const double b = gi_cons_b(C, id);
+    dj = 0.0;
+    if (id < 2 * nf) {
+        const int a = id < nf ? id : id - nf;
+        const double sg = id < nf ? 1.0 : -1.0;
+        if (ln < nf) dj = sg * L.J[ln * ld + a];
+        sp = sg * readlane(x, a) - b;
+    } else if (id < 2 * nf + nfric) {
+        const int r = id - 2 * nf, ks = r >> 2, t = r & 3;
+        const int k = ks / P.nfeet, sft = ks % P.nfeet;
+        const int pz = L.pos[k * P.nu + 3 * sft + 2], pt = L.pos[k * P.nu + 3 * sft + (t >> 1)];
+        const double sg = (t & 1) ? 1.0 : -1.0;
+        double nx_ = 0.0;
+        if (pz >= 0) { if (ln < nf) dj += P.mu * L.J[ln * ld + pz]; nx_ += P.mu * readlane(x, pz); }
+        if (pt >= 0) { if (ln < nf) dj += sg * L.J[ln * ld + pt]; nx_ += sg * readlane(x, pt); }
+        sp = nx_ - b;
+    } else {
+        const int r = id - 2 * nf - nfric, row = r >> 1, side = r & 1;
+        const double sg = side ? -1.0 : 1.0;
+        double acc = 0.0, part = 0.0;
+        for (int a = 0; a < nf; ++a) {
+            const double na = sg * rowA(P, row, L.fid[a]);
+            if (ln < nf) acc += L.J[ln * ld + a] * na;
+        }
+        for (int a = ln; a < nf; a += kWave) part += sg * rowA(P, row, L.fid[a]) * L.xs[a];
+        dj = acc;
+        sp = wave_sum(part) - b;
+    }
+}
+
+// ---------------------------------------------------------------- stage 1: setup
+// Fixed variables, free index map, constraint states.  Leaves C.nf, C.mt, C.status.
+__device__ inline void gi_setup(GiCtx &C) {
+    const SolveProblem &P = *C.P;
+    GiLds &L = C.L;
+    const int nV = P.nV, mA = P.mA, ln = lane(), nfmax = C.nfmax;
+    C.nfric = P.friction ? 4 * P.N * P.nfeet : 0;
+    C.status = ST_OK;
+    C.c0 = 0.0;
     int nf = 0;
     for (int base = 0; base < nV; base += kWave) {
         const int v = base + ln;
@@ -133,7 +231,7 @@ __device__ inline void wave_gi_solve(const SolveProblem &P, const SolveOut &O,
         if (valid) var_bounds(P, v, lo, hi);
         const bool bad = valid && lo > hi;
         const bool freev = valid && lo != hi;
-        if (__any(bad)) status = ST_INFEASIBLE;
+        if (__any(bad)) C.status = ST_INFEASIBLE;
         const unsigned long long m = __ballot(freev);
         const int before = __popcll(m & ((1ull << ln) - 1ull));
         if (valid) {
@@ -144,128 +242,101 @@ __device__ inline void wave_gi_solve(const SolveProblem &P, const SolveOut &O,
         nf += __popcll(m);
     }
     wave_sync();
-    if (nf > nfmax || nf > kWave) status = ST_BAD_DIMS;
+    C.nf = nf;
+    if (nf > nfmax || nf > kWave) C.status = ST_BAD_DIMS;
+    const int nfric = C.nfric;
     const int mt = 2 * nf + nfric + 2 * mA;
-
-    // b of the one-sided constraint id (normal' x_F >= b, fixed parts folded into b)
-    auto cons_b = [&](int id) -> double {
-        double lo, hi;
-        if (id < nf) { var_bounds(P, L.fid[id], lo, hi); return lo; }
-        if (id < 2 * nf) { var_bounds(P, L.fid[id - nf], lo, hi); return -hi; }
-        if (id < 2 * nf + nfric) {
+    C.mt = mt;
+    if (C.status != ST_OK) return;
+    for (int id = ln; id < mt; id += kWave) {
+        unsigned char s = 0;
+        if (id < 2 * nf) {
+            double lo, hi;
+            var_bounds(P, L.fid[id < nf ? id : id - nf], lo, hi);
+            s = (id < nf) ? (lo > -kInfty ? 1 : 0) : (hi < kInfty ? 1 : 0);
+        } else if (id < 2 * nf + nfric) {
             const int r = id - 2 * nf, ks = r >> 2, t = r & 3;
             const int k = ks / P.nfeet, sft = ks % P.nfeet;
-            const int vz = k * P.nu + 3 * sft + 2, vt = k * P.nu + 3 * sft + (t >> 1);
-            const double sg = (t & 1) ? 1.0 : -1.0;
-            double b = 0.0;
-            if (L.pos[vz] < 0) b -= P.mu * L.xfull[vz];
-            if (L.pos[vt] < 0) b -= sg * L.xfull[vt];
-            return b;
-        }
-        const int r = id - 2 * nf - nfric, row = r >> 1, side = r & 1;
-        return side ? (-P.ubA[row] + L.rowfix[row]) : (P.lbA[row] - L.rowfix[row]);
-    };
-    // slack n'x - b of constraint id evaluated by ONE lane (x read from the LDS mirror)
-    auto cons_slack_lane = [&](int id) -> double {
-        if (id < nf) return L.xs[id] - cons_b(id);
-        if (id < 2 * nf) return -L.xs[id - nf] - cons_b(id);
-        if (id < 2 * nf + nfric) {
-            const int r = id - 2 * nf, ks = r >> 2, t = r & 3;
-            const int k = ks / P.nfeet, sft = ks % P.nfeet;
-            const int vz = k * P.nu + 3 * sft + 2, vt = k * P.nu + 3 * sft + (t >> 1);
-            const double sg = (t & 1) ? 1.0 : -1.0;
-            const int pz = L.pos[vz], pt = L.pos[vt];
-            double s = 0.0;
-            if (pz >= 0) s += P.mu * L.xs[pz];
-            if (pt >= 0) s += sg * L.xs[pt];
-            return s - cons_b(id);
-        }
-        const int r = id - 2 * nf - nfric, row = r >> 1, side = r & 1;
-        const double sg = side ? -1.0 : 1.0;
-        double s = 0.0;
-        for (int a = 0; a < nf; ++a) s += sg * rowA(P, row, L.fid[a]) * L.xs[a];
-        return s - cons_b(id);
-    };
-
-    if (status == ST_OK) {
-        // ---- constraint states
-        for (int id = ln; id < mt; id += kWave) {
-            unsigned char s = 0;
-            if (id < 2 * nf) {
-                double lo, hi;
-                var_bounds(P, L.fid[id < nf ? id : id - nf], lo, hi);
-                s = (id < nf) ? (lo > -kInfty ? 1 : 0) : (hi < kInfty ? 1 : 0);
-            } else if (id < 2 * nf + nfric) {
-                const int r = id - 2 * nf, ks = r >> 2, t = r & 3;
-                const int k = ks / P.nfeet, sft = ks % P.nfeet;
-                if ((P.contact >> (2 * k + sft)) & 1ull) {
-                    const int vz = k * P.nu + 3 * sft + 2, vt = k * P.nu + 3 * sft + (t >> 1);
-                    const double sg = (t & 1) ? 1.0 : -1.0;
-                    if (L.pos[vz] >= 0 || L.pos[vt] >= 0) s = 1;
-                    else {
-                        const double bb = -(P.mu * L.xfull[vz] + sg * L.xfull[vt]);
-                        if (bb > kFeasTol * (1.0 + fabs(bb))) s = 4;  // 0 >= b violated
-                    }
+            if ((P.contact >> (2 * k + sft)) & 1ull) {
+                const int vz = k * P.nu + 3 * sft + 2, vt = k * P.nu + 3 * sft + (t >> 1);
+                const double sg = (t & 1) ? 1.0 : -1.0;
+                if (L.pos[vz] >= 0 || L.pos[vt] >= 0) s = 1;
+                else {
+                    const double bb = -(P.mu * L.xfull[vz] + sg * L.xfull[vt]);
+                    if (bb > kFeasTol * (1.0 + fabs(bb))) s = 4;  // 0 >= b violated
                 }
-            } else {
-                const int r = id - 2 * nf - nfric, row = r >> 1, side = r & 1;
-                const double lo = P.lbA ? P.lbA[row] : -kInfty, hi = P.ubA ? P.ubA[row] : kInfty;
-                bool anyfree = false;
-                double fix = 0.0;
-                for (int v = 0; v < nV; ++v) {
-                    const double a = rowA(P, row, v);
-                    if (L.pos[v] >= 0) anyfree |= (a != 0.0);
-                    else fix += a * L.xfull[v];
-                }
-                if (side == 0) L.rowfix[row] = fix;
-                if (lo > hi) s = 4;
-                else if (!anyfree) {
-                    bool ok = true;
-                    if (lo == hi) { const double bb = lo - fix; ok = fabs(bb) <= kFeasTol * (1.0 + fabs(bb)); }
-                    else if (side == 0 && lo > -kInfty) { const double bb = lo - fix; ok = !(bb > kFeasTol * (1.0 + fabs(bb))); }
-                    else if (side == 1 && hi < kInfty) { const double bb = fix - hi; ok = !(bb > kFeasTol * (1.0 + fabs(bb))); }
-                    s = ok ? 0 : 4;
-                } else if (lo == hi) s = side == 0 ? 3 : 0;
-                else if (side == 0) s = lo > -kInfty ? 1 : 0;
-                else s = hi < kInfty ? 1 : 0;
             }
-            L.st[id] = s;
+        } else {
+            const int r = id - 2 * nf - nfric, row = r >> 1, side = r & 1;
+            const double lo = P.lbA ? P.lbA[row] : -kInfty, hi = P.ubA ? P.ubA[row] : kInfty;
+            bool anyfree = false;
+            double fix = 0.0;
+            for (int v = 0; v < nV; ++v) {
+                const double a = rowA(P, row, v);
+                if (L.pos[v] >= 0) anyfree |= (a != 0.0);
+                else fix += a * L.xfull[v];
+            }
+            if (side == 0) L.rowfix[row] = fix;
+            if (lo > hi) s = 4;
+            else if (!anyfree) {
+                bool ok = true;
+                if (lo == hi) { const double bb = lo - fix; ok = fabs(bb) <= kFeasTol * (1.0 + fabs(bb)); }
+                else if (side == 0 && lo > -kInfty) { const double bb = lo - fix; ok = !(bb > kFeasTol * (1.0 + fabs(bb))); }
+                else if (side == 1 && hi < kInfty) { const double bb = fix - hi; ok = !(bb > kFeasTol * (1.0 + fabs(bb))); }
+                s = ok ? 0 : 4;
+            } else if (lo == hi) s = side == 0 ? 3 : 0;
+            else if (side == 0) s = lo > -kInfty ? 1 : 0;
+            else s = hi < kInfty ? 1 : 0;
         }
-        wave_sync();
-        bool infe = false;
-        for (int id = ln; id < mt; id += kWave) infe |= (L.st[id] == 4);
-        if (__any(infe)) status = ST_INFEASIBLE;
+        L.st[id] = s;
     }
+    wave_sync();
+    bool infe = false;
+    for (int id = ln; id < mt; id += kWave) infe |= (L.st[id] == 4);
+    if (__any(infe)) C.status = ST_INFEASIBLE;
+}
 
-    double fval = 0.0, c0 = 0.0;
-    int iters = 0, q = 0;
-    double x = 0.0;  // lane i: x_i (free position i)
+// ---------------------------------------------------------------- stage 2: gather
+// H_FF (lower triangle suffices) into R, g = f_F + H_FB x_B, c0 = fixed-part objective.
+__device__ inline void gi_gather(GiCtx &C) {
+    const SolveProblem &P = *C.P;
+    GiLds &L = C.L;
+    const int nV = P.nV, nf = C.nf, ld = L.ld, ln = lane();
+    if (C.status != ST_OK) return;
+    for (int b = 0; b < nf; ++b) {
+        const int vb = L.fid[b];
+        for (int a = ln; a < nf; a += kWave) L.R[b * ld + a] = P.H[(size_t)vb * nV + L.fid[a]];
+    }
+    for (int a = ln; a < nf; a += kWave) {
+        const int va = L.fid[a];
+        double s = P.f[va];
+        for (int j = 0; j < nV; ++j)
+            if (L.pos[j] < 0 && L.xfull[j] != 0.0) s += P.H[(size_t)j * nV + va] * L.xfull[j];
+        L.g[a] = s;
+    }
+    double cl = 0.0;
+    for (int i = ln; i < nV; i += kWave)
+        if (L.pos[i] < 0 && L.xfull[i] != 0.0) {
+            double s = 0.0;
+            for (int j = 0; j < nV; ++j)
+                if (L.pos[j] < 0) s += P.H[(size_t)j * nV + i] * L.xfull[j];
+            cl += 0.5 * L.xfull[i] * s + P.f[i] * L.xfull[i];
+        }
+    C.c0 = wave_sum(cl);
+    wave_sync();
+}
+
+// ---------------------------------------------------------------- stage 3: factor + loop
+__device__ inline void gi_run(GiCtx &C) {
+    const SolveProblem &P = *C.P;
+    GiLds &L = C.L;
+    const int nf = C.nf, ld = L.ld, ln = lane(), mt = C.mt, nfric = C.nfric;
+    double fval = 0.0, x = 0.0, u = 0.0;
+    int iters = 0, q = 0, act = -1, eqs = 0;
+    int status = C.status;
 
     if (status == ST_OK && nf > 0) {
-        // ---- reduced Hessian H_FF into R (scratch), gradient g = f_F + H_FB x_B, const c0
-        for (int b = 0; b < nf; ++b) {
-            const int vb = L.fid[b];
-            for (int a = ln; a < nf; a += kWave) L.R[b * ld + a] = P.H[(size_t)vb * nV + L.fid[a]];
-        }
-        for (int a = ln; a < nf; a += kWave) {
-            const int va = L.fid[a];
-            double s = P.f[va];
-            for (int j = 0; j < nV; ++j)
-                if (L.pos[j] < 0 && L.xfull[j] != 0.0) s += P.H[(size_t)j * nV + va] * L.xfull[j];
-            L.g[a] = s;
-        }
-        double cl = 0.0;
-        for (int i = ln; i < nV; i += kWave)
-            if (L.pos[i] < 0 && L.xfull[i] != 0.0) {
-                double s = 0.0;
-                for (int j = 0; j < nV; ++j)
-                    if (L.pos[j] < 0) s += P.H[(size_t)j * nV + i] * L.xfull[j];
-                cl += 0.5 * L.xfull[i] * s + P.f[i] * L.xfull[i];
-            }
-        c0 = wave_sum(cl);
-        wave_sync();
-
-        // ---- Cholesky H_FF = L L' in place (lower), left-looking by column
+        // Cholesky H_FF = L L' in place (lower), left-looking by column
         for (int k = 0; k < nf; ++k) {
             double piv = L.R[k * ld + k];
             for (int l = 0; l < k; ++l) piv -= L.R[l * ld + k] * L.R[l * ld + k];
@@ -281,19 +352,21 @@ __device__ inline void wave_gi_solve(const SolveProblem &P, const SolveOut &O,
             wave_sync();
         }
     } else if (status == ST_OK) {
-        // nothing free: cost of the fixed point
+        // nothing free: cost of the fixed point only
+        const int nV = P.nV;
         double cl = 0.0;
-        for (int i = ln; i < nV; i += kWave) {
-            double s = 0.0;
-            for (int j = 0; j < nV; ++j) s += P.H[(size_t)j * nV + i] * L.xfull[j];
-            cl += 0.5 * L.xfull[i] * s + P.f[i] * L.xfull[i];
-        }
-        c0 = wave_sum(cl);
+        if (P.H)
+            for (int i = ln; i < nV; i += kWave) {
+                double s = 0.0;
+                for (int j = 0; j < nV; ++j) s += P.H[(size_t)j * nV + i] * L.xfull[j];
+                cl += 0.5 * L.xfull[i] * s + P.f[i] * L.xfull[i];
+            }
+        C.c0 = wave_sum(cl);
     }
 
     if (status == ST_OK && nf > 0) {
-        // ---- J = L^-T: lane c computes column c of L^-1 and stores Linv(i, c) at
-        //      J[i*ld + c], which is J(c, i) in column-major order.
+        // J = L^-T: lane c computes column c of L^-1 and stores Linv(i, c) at J[i*ld + c],
+        // which is J(c, i) in column-major order.
         for (int c = ln; c < nf; c += kWave) {
             for (int i = 0; i < c; ++i) L.J[i * ld + c] = 0.0;
             for (int i = c; i < nf; ++i) {
@@ -303,7 +376,7 @@ __device__ inline void wave_gi_solve(const SolveProblem &P, const SolveOut &O,
             }
         }
         wave_sync();
-        // ---- unconstrained minimum x = -J J' g
+        // unconstrained minimum x = -J J' g
         double w = 0.0;
         if (ln < nf)
             for (int i = 0; i < nf; ++i) w += L.J[ln * ld + i] * L.g[i];
@@ -318,45 +391,8 @@ __device__ inline void wave_gi_solve(const SolveProblem &P, const SolveOut &O,
         wave_sync();
     }
 
-    // ---- Goldfarb-Idnani loop
-    double u = 0.0;   // lane j: multiplier of slot j (slot q: the candidate's)
-    int act = -1;     // lane j: constraint id in slot j
-    int eqs = 0;      // lane j: slot holds an equality
     const int max_iter = P.max_iter > 0 ? P.max_iter : 10 * (mt + nf + 1);
     int eq_next = 2 * nf + nfric;  // dense rows are the only equality candidates
-
-    // d_j = (J' n_p)_j on lane j, and the slack n_p'x - b (uniform)
-    auto cons_project = [&](int id, double &dj, double &sp) {
-        const double b = cons_b(id);
-        dj = 0.0;
-        if (id < 2 * nf) {
-            const int a = id < nf ? id : id - nf;
-            const double sg = id < nf ? 1.0 : -1.0;
-            if (ln < nf) dj = sg * L.J[ln * ld + a];
-            sp = sg * readlane(x, a) - b;
-        } else if (id < 2 * nf + nfric) {
-            const int r = id - 2 * nf, ks = r >> 2, t = r & 3;
-            const int k = ks / P.nfeet, sft = ks % P.nfeet;
-            const int pz = L.pos[k * P.nu + 3 * sft + 2], pt = L.pos[k * P.nu + 3 * sft + (t >> 1)];
-            const double sg = (t & 1) ? 1.0 : -1.0;
-            double nx_ = 0.0;
-            if (pz >= 0) { if (ln < nf) dj += P.mu * L.J[ln * ld + pz]; nx_ += P.mu * readlane(x, pz); }
-            if (pt >= 0) { if (ln < nf) dj += sg * L.J[ln * ld + pt]; nx_ += sg * readlane(x, pt); }
-            sp = nx_ - b;
-        } else {
-            const int r = id - 2 * nf - nfric, row = r >> 1, side = r & 1;
-            const double sg = side ? -1.0 : 1.0;
-            double acc = 0.0, part = 0.0;
-            for (int a = 0; a < nf; ++a) {
-                const double na = sg * rowA(P, row, L.fid[a]);
-                if (ln < nf) acc += L.J[ln * ld + a] * na;
-            }
-            for (int a = ln; a < nf; a += kWave) part += sg * rowA(P, row, L.fid[a]) * L.xs[a];
-            dj = acc;
-            sp = wave_sum(part) - b;
-        }
-    };
-
     bool done = (status != ST_OK) || nf == 0;
     while (!done) {
         // ---- step 1: the constraint to add (pending equalities first, in row order)
@@ -373,15 +409,15 @@ __device__ inline void wave_gi_solve(const SolveProblem &P, const SolveOut &O,
             int bid = 0x7fffffff;
             for (int id = ln; id < mt; id += kWave) {
                 if (L.st[id] != 1) continue;
-                const double s = cons_slack_lane(id);
-                if (s < -kFeasTol * (1.0 + fabs(cons_b(id))) && s < best) { best = s; bid = id; }
+                const double s = gi_cons_slack_lane(C, id);
+                if (s < -kFeasTol * (1.0 + fabs(gi_cons_b(C, id))) && s < best) { best = s; bid = id; }
             }
             wave_argmin(best, bid);
             if (bid == 0x7fffffff) break;  // optimal
             p = bid;
         }
         double dj;
-        cons_project(p, dj, sp);
+        gi_cons_project(C, p, x, dj, sp);
         if (ln == q) u = 0.0;
         // ---- step 2
         for (;;) {
@@ -409,7 +445,7 @@ __device__ inline void wave_gi_solve(const SolveProblem &P, const SolveOut &O,
             wave_argmin(t1, kslot);
             const bool dep = !(zn > kDepTol * dd);
             if (adding_eq && dep) {
-                const double bp = cons_b(p);
+                const double bp = gi_cons_b(C, p);
                 if (fabs(sp) <= kFeasTol * (1.0 + fabs(bp))) break;  // consistent: skip
                 status = ST_INFEASIBLE; done = true; break;
             }
@@ -496,29 +532,42 @@ __device__ inline void wave_gi_solve(const SolveProblem &P, const SolveOut &O,
                 wave_sync();
             }
             // p remains the target: refresh d and its slack
-            cons_project(p, dj, sp);
+            gi_cons_project(C, p, x, dj, sp);
         }
     }
+    C.status = status;
+    C.x = x;
+    C.u = u;
+    C.fval = fval;
+    C.act = act;
+    C.q = q;
+    C.iters = iters;
+}
 
-    // ---- outputs
-    const bool have_map = nf <= nfmax && nf <= kWave;
+// ---------------------------------------------------------------- stage 4: outputs
+__device__ inline void gi_write(GiCtx &C, const SolveOut &O) {
+    const SolveProblem &P = *C.P;
+    GiLds &L = C.L;
+    const int nV = P.nV, mA = P.mA, nf = C.nf, ln = lane(), nfric = C.nfric;
+    const bool have_map = nf <= C.nfmax && nf <= kWave;
     for (int v = ln; v < nV; v += kWave) {
         const int pv = L.pos[v];
         if (pv < 0 || !have_map) O.x[v] = (pv < 0) ? L.xfull[v] : 0.0;
     }
-    if (have_map && ln < nf) O.x[L.fid[ln]] = x;
+    if (have_map && ln < nf) O.x[L.fid[ln]] = C.x;
     if (ln == 0) {
-        *O.cost = fval + c0;
-        *O.status = status;
-        *O.iters = iters;
+        *O.cost = C.fval + C.c0;
+        *O.status = C.status;
+        *O.iters = C.iters;
     }
     if (O.y) {
         // multipliers: y_b (nV) then y_A (mA) with H x + f = y_b + A' y_A, built in LDS
         for (int v = ln; v < nV + mA; v += kWave) L.ys[v] = 0.0;
-        if (have_map && ln < nf) L.xfull[L.fid[ln]] = x;  // full primal vector in LDS
+        if (have_map && ln < nf) L.xfull[L.fid[ln]] = C.x;  // full primal vector in LDS
         wave_sync();
-        if (status == ST_OK && ln < q) {
-            const int id = act;
+        if (C.status == ST_OK && ln < C.q) {
+            const int id = C.act;
+            const double u = C.u;
             if (id < nf) L.ys[L.fid[id]] = u;
             else if (id < 2 * nf) L.ys[L.fid[id - nf]] = -u;
             else if (id >= 2 * nf + nfric) {
@@ -537,6 +586,19 @@ __device__ inline void wave_gi_solve(const SolveProblem &P, const SolveOut &O,
         wave_sync();
         for (int v = ln; v < nV + mA; v += kWave) O.y[v] = L.ys[v];
     }
+}
+
+// Stand-alone solve of one instance from H, f in global memory (LDS: gi_lds_bytes).
+__device__ inline void wave_gi_solve(const SolveProblem &P, const SolveOut &O,
+                                     unsigned char *smem, int nfmax) {
+    GiCtx C;
+    C.P = &P;
+    C.L = gi_carve(smem, nfmax, P.nV, P.mA);
+    C.nfmax = nfmax;
+    gi_setup(C);
+    gi_gather(C);
+    gi_run(C);
+    gi_write(C, O);
 }
 
 }  // namespace mpcqp

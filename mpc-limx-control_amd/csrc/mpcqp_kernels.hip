@@ -7,6 +7,8 @@
 //                arrays A_eq, b_eq, lb, ub, A_ineq, lbA, ubA).        src/QPSolver.cpp:21-81,
 //                include/mpcQP.h:121-182
 //   k_solve      corrected dense QP, Goldfarb-Idnani                  src/QPSolver.cpp:83-106
+//   k_discretize<..>, k_condense_solve<..>   the batched hot path with compile-time dims
+//                (fused.hpp): linearise + expm, then Phi, H_FF, f and the solve in LDS
 //   k_select_min per-rank min-cost key (multi-GPU selection)
 //   k_plant      x <- Ad x + Bd u                                       src/QPSolver.cpp:108-111
 #include <hip/hip_runtime.h>
@@ -20,6 +22,7 @@
 
 #include "../../include/mpcqp.h"
 #include "condense.hpp"
+#include "fused.hpp"
 #include "gi_solver.hpp"
 
 using namespace mpcqp;
@@ -192,6 +195,56 @@ __global__ void __launch_bounds__(64) k_plant(int nx, int nu, const double *Ad, 
     }
 }
 
+// ------------------------------------------------------------------ fast path kernels
+template <int NX, int NU, int MODEL>
+__global__ void __launch_bounds__(64) k_discretize(FastArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem_f[];
+    if ((int)blockIdx.x >= a.B) return;
+    fast_discretize<NX, NU, MODEL>(a, smem_f);
+}
+
+template <int NX, int NU, int N, int MODEL, bool FRIC, int NFMAX>
+__global__ void __launch_bounds__(64) k_condense_solve(FastArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_c[];
+    if ((int)blockIdx.x >= a.B) return;
+    fast_condense_solve<NX, NU, N, MODEL, FRIC, NFMAX>(a, smem_c);
+}
+
+struct FastKernels {
+    const void *disc = nullptr, *cs = nullptr;
+    size_t disc_lds = 0, cs_lds = 0;
+    int nx = 0, nu = 0;
+};
+
+template <int NX, int NU, int N, int MODEL, bool FRIC, int NFMAX>
+FastKernels make_fast() {
+    FastKernels k;
+    k.disc = (const void *)&k_discretize<NX, NU, MODEL>;
+    k.cs = (const void *)&k_condense_solve<NX, NU, N, MODEL, FRIC, NFMAX>;
+    k.disc_lds = sizeof(double) * disc_lds_doubles<NX, NU>();
+    k.cs_lds = CSLayout<NX, NU, N, FRIC, NFMAX>::lds_bytes;
+    k.nx = NX;
+    k.nu = NU;
+    return k;
+}
+
+// instantiated configurations (BASELINE configs A/B/C and the literal model); anything else
+// runs the generic runtime-dimension kernels
+bool pick_fast(int model, int nx, int nu, int N, bool fric, int nfmax, FastKernels &k) {
+    if (nx != 13) return false;
+    if (model == MPCQP_MODEL_SRBM && nu == 6) {
+        if (N == 10 && nfmax <= 32) { k = fric ? make_fast<13, 6, 10, 0, true, 32>() : make_fast<13, 6, 10, 0, false, 32>(); return true; }
+        if (N == 10 && nfmax <= 64) { k = fric ? make_fast<13, 6, 10, 0, true, 64>() : make_fast<13, 6, 10, 0, false, 64>(); return true; }
+        if (N == 20 && nfmax <= 64) { k = fric ? make_fast<13, 6, 20, 0, true, 64>() : make_fast<13, 6, 20, 0, false, 64>(); return true; }
+        return false;
+    }
+    if (model == MPCQP_MODEL_LITERAL && nu == 3 && !fric) {
+        if (N == 20 && nfmax <= 64) { k = make_fast<13, 3, 20, 1, false, 64>(); return true; }
+        if (N == 10 && nfmax <= 32) { k = make_fast<13, 3, 10, 1, false, 32>(); return true; }
+    }
+    return false;
+}
+
 // ------------------------------------------------------------------------------ host side
 void inv3(const double *A, double *Ai) {  // same formula as the oracle's model builder
     const double a = A[0], b = A[3], c = A[6], d = A[1], e = A[4], f = A[7], g = A[2],
@@ -264,6 +317,12 @@ struct mpcqp_ctx {
     bool ev_used[3] = {false, false, false};
     double *scratchH = nullptr, *scratchF = nullptr;
     size_t scratch_cap = 0;
+    // fast path
+    bool fast = false;
+    FastKernels fk;
+    double *dqd = nullptr, *dpd = nullptr;  // diagonals of Q, P
+    double *dAB = nullptr;                  // [B][nx*(nx+nu)] discretised model scratch
+    size_t ab_cap = 0;
 };
 
 extern "C" {
@@ -469,6 +528,13 @@ out:
 }
 
 // ------------------------------------------------------------------------- batched path
+static bool is_diag(const double *M, int n) {
+    for (int j = 0; j < n; ++j)
+        for (int i = 0; i < n; ++i)
+            if (i != j && M[j * n + i] != 0.0) return false;
+    return true;
+}
+
 int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
     if (!m || !out || !m->Q || !m->R || !m->P) return MPCQP_ERR_BAD_ARG;
     *out = nullptr;
@@ -489,17 +555,30 @@ int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
     c->device = device;
     inv3(m->Ib, c->Ibinv);
     const int nx = m->nx, nu = m->nu;
+    double qd[MPCQP_MAX_NX], pd[MPCQP_MAX_NX];
+    for (int i = 0; i < nx; ++i) { qd[i] = m->Q[i * nx + i]; pd[i] = m->P[i * nx + i]; }
     if (hipMalloc(&c->dQ, sizeof(double) * nx * nx) != hipSuccess ||
         hipMalloc(&c->dR, sizeof(double) * nu * nu) != hipSuccess ||
         hipMalloc(&c->dP, sizeof(double) * nx * nx) != hipSuccess ||
+        hipMalloc(&c->dqd, sizeof(double) * nx) != hipSuccess ||
+        hipMalloc(&c->dpd, sizeof(double) * nx) != hipSuccess ||
         hipMemcpy(c->dQ, m->Q, sizeof(double) * nx * nx, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->dR, m->R, sizeof(double) * nu * nu, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->dP, m->P, sizeof(double) * nx * nx, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->dqd, qd, sizeof(double) * nx, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(c->dpd, pd, sizeof(double) * nx, hipMemcpyHostToDevice) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         mpcqp_ctx_destroy(c);
         return MPCQP_ERR_DEVICE;
     }
     c->own_stream = true;
+    // fast path: compile-time dims, diagonal Q/P (the reference's asDiagonal() weights,
+    // include/mpcQP.h:54-56), and in-contact forces never fixed (so fixed inputs are 0)
+    const bool fric = m->model == MPCQP_MODEL_SRBM && m->constraints == MPCQP_CONS_FRICTION;
+    const bool bounds_ok = m->model == MPCQP_MODEL_LITERAL ||
+                           (m->fz_min < m->fz_max && m->fxy_max > 0.0);
+    c->fast = is_diag(m->Q, nx) && is_diag(m->P, nx) && bounds_ok && nu <= 6 &&
+              pick_fast(m->model, nx, nu, m->N, fric, nfmax, c->fk);
     c->m.Q = c->m.R = c->m.P = nullptr;  // host pointers are not kept
     c->ev_ok = true;
     for (int i = 0; i < 6; ++i)
@@ -508,6 +587,8 @@ int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
     return MPCQP_OK;
 }
 
+int mpcqp_ctx_fast_path(const mpcqp_ctx *c) { return c && c->fast ? 1 : 0; }
+
 int mpcqp_ctx_destroy(mpcqp_ctx *c) {
     if (!c) return MPCQP_ERR_BAD_ARG;
     hipSetDevice(c->device);
@@ -515,6 +596,9 @@ int mpcqp_ctx_destroy(mpcqp_ctx *c) {
     hipFree(c->dQ);
     hipFree(c->dR);
     hipFree(c->dP);
+    hipFree(c->dqd);
+    hipFree(c->dpd);
+    hipFree(c->dAB);
     hipFree(c->scratchH);
     hipFree(c->scratchF);
     if (c->ev_ok)
@@ -554,6 +638,13 @@ double mpcqp_last_kernel_ms(mpcqp_ctx *c, int which) {
     return ms;
 }
 
+static void tbegin(mpcqp_ctx *c, int which) {
+    if (c->timing) hipEventRecord(c->ev[2 * which], c->stream);
+}
+static void tend(mpcqp_ctx *c, int which) {
+    if (c->timing) { hipEventRecord(c->ev[2 * which + 1], c->stream); c->ev_used[which] = true; }
+}
+
 static CondenseArgs batch_condense_args(mpcqp_ctx *c, int B, const double *x0, const double *xref,
                                         const double *lin, double *H, double *f) {
     CondenseArgs a;
@@ -569,6 +660,33 @@ static CondenseArgs batch_condense_args(mpcqp_ctx *c, int B, const double *x0, c
     return a;
 }
 
+static FastArgs fast_args(mpcqp_ctx *c, int B) {
+    FastArgs a;
+    memset(&a, 0, sizeof(a));
+    const mpcqp_model &m = c->m;
+    a.B = B;
+    a.Ts = m.Ts;
+    a.mass = m.mass;
+    for (int i = 0; i < 9; ++i) a.Ibinv[i] = c->Ibinv[i];
+    a.qd = c->dqd;
+    a.pd = c->dpd;
+    a.rmat = c->dR;
+    a.fz_min = m.fz_min;
+    a.fz_max = m.fz_max;
+    a.fxy_max = m.fxy_max;
+    a.u_min = m.u_min;
+    a.u_max = m.u_max;
+    a.mu = m.mu;
+    a.max_iter = m.max_iter;
+    a.max_free = m.max_free > 0 ? m.max_free : m.nu * m.N;
+    return a;
+}
+
+static int launch(const void *k, int B, size_t lds, hipStream_t s, void *arg) {
+    void *args[] = {arg};
+    return hip_status(hipLaunchKernel(k, dim3(B), dim3(64), args, lds, s));
+}
+
 int mpcqp_batch_condense(mpcqp_ctx *c, int B, const double *x0, const double *xref,
                          const double *lin, double *H, double *f) {
     if (!c || !x0 || !xref || !lin || !H || !f || B < 0) return MPCQP_ERR_BAD_ARG;
@@ -577,19 +695,15 @@ int mpcqp_batch_condense(mpcqp_ctx *c, int B, const double *x0, const double *xr
     CondenseArgs a = batch_condense_args(c, B, x0, xref, lin, H, f);
     const size_t lds = set_lds((const void *)k_condense,
                                sizeof(double) * condense_lds_doubles(c->m.nx, c->m.nu, c->m.N));
-    if (c->timing) hipEventRecord(c->ev[0], c->stream);
+    tbegin(c, 0);
     hipLaunchKernelGGL(k_condense, dim3(B), dim3(64), lds, c->stream, a);
-    if (c->timing) { hipEventRecord(c->ev[1], c->stream); c->ev_used[0] = true; }
+    tend(c, 0);
     return hip_status(hipGetLastError());
 }
 
-int mpcqp_batch_solve_qp(mpcqp_ctx *c, int B, const double *H, const double *f,
-                         const uint64_t *contact, double *U, double *cost, int *status,
-                         int *iters) {
-    if (!c || !H || !f || !U || !cost || !status || !iters || B < 0) return MPCQP_ERR_BAD_ARG;
-    if (c->m.model == MPCQP_MODEL_SRBM && !contact) return MPCQP_ERR_BAD_ARG;
-    if (B == 0) return MPCQP_OK;
-    hipSetDevice(c->device);
+static SolveArgs batch_solve_args(mpcqp_ctx *c, int B, const double *H, const double *f,
+                                  const uint64_t *contact, double *U, double *cost, int *status,
+                                  int *iters) {
     SolveArgs a;
     memset(&a, 0, sizeof(a));
     const mpcqp_model &m = c->m;
@@ -616,12 +730,97 @@ int mpcqp_batch_solve_qp(mpcqp_ctx *c, int B, const double *H, const double *f,
     a.cost = cost;
     a.status = status;
     a.iters = iters;
-    const int nfric = a.P.friction ? 4 * m.N * 2 : 0;
+    return a;
+}
+
+int mpcqp_batch_solve_qp(mpcqp_ctx *c, int B, const double *H, const double *f,
+                         const uint64_t *contact, double *U, double *cost, int *status,
+                         int *iters) {
+    if (!c || !H || !f || !U || !cost || !status || !iters || B < 0) return MPCQP_ERR_BAD_ARG;
+    if (c->m.model == MPCQP_MODEL_SRBM && !contact) return MPCQP_ERR_BAD_ARG;
+    if (B == 0) return MPCQP_OK;
+    hipSetDevice(c->device);
+    SolveArgs a = batch_solve_args(c, B, H, f, contact, U, cost, status, iters);
+    const int nfric = a.P.friction ? 4 * c->m.N * 2 : 0;
     const size_t lds = set_lds((const void *)k_solve, gi_lds_bytes(a.nfmax, a.P.nV, 0, nfric));
-    if (c->timing) hipEventRecord(c->ev[2], c->stream);
+    tbegin(c, 1);
     hipLaunchKernelGGL(k_solve, dim3(B), dim3(64), lds, c->stream, a);
-    if (c->timing) { hipEventRecord(c->ev[3], c->stream); c->ev_used[1] = true; }
+    tend(c, 1);
     return hip_status(hipGetLastError());
+}
+
+int mpcqp_batch_discretize(mpcqp_ctx *c, int B, const double *lin, double *AB) {
+    if (!c || !lin || !AB || B < 0) return MPCQP_ERR_BAD_ARG;
+    if (B == 0) return MPCQP_OK;
+    hipSetDevice(c->device);
+    int rc;
+    tbegin(c, 0);
+    if (c->fast) {
+        FastArgs a = fast_args(c, B);
+        a.lin = lin;
+        a.AB = AB;
+        rc = launch(c->fk.disc, B, c->fk.disc_lds, c->stream, &a);
+    } else {
+        CondenseArgs a = batch_condense_args(c, B, nullptr, nullptr, lin, nullptr, nullptr);
+        a.ABout = AB;
+        a.discretize_only = 1;
+        const size_t lds = set_lds((const void *)k_condense,
+                                   sizeof(double) * condense_lds_doubles(c->m.nx, c->m.nu, 1));
+        hipLaunchKernelGGL(k_condense, dim3(B), dim3(64), lds, c->stream, a);
+        rc = hip_status(hipGetLastError());
+    }
+    tend(c, 0);
+    return rc;
+}
+
+static int ensure_scratch_hf(mpcqp_ctx *c, int B) {
+    const size_t nV = (size_t)c->m.nu * c->m.N;
+    if (c->scratch_cap >= (size_t)B) return MPCQP_OK;
+    hipFree(c->scratchH);
+    hipFree(c->scratchF);
+    c->scratchH = c->scratchF = nullptr;
+    c->scratch_cap = 0;
+    if (hipMalloc(&c->scratchH, sizeof(double) * nV * nV * B) != hipSuccess ||
+        hipMalloc(&c->scratchF, sizeof(double) * nV * B) != hipSuccess)
+        return MPCQP_ERR_DEVICE;
+    c->scratch_cap = B;
+    return MPCQP_OK;
+}
+
+int mpcqp_batch_condense_solve(mpcqp_ctx *c, int B, const double *AB, const double *x0,
+                               const double *xref, const uint64_t *contact, double *U,
+                               double *cost, int *status, int *iters) {
+    if (!c || !AB || !x0 || !xref || !U || !cost || !status || !iters || B < 0)
+        return MPCQP_ERR_BAD_ARG;
+    if (c->m.model == MPCQP_MODEL_SRBM && !contact) return MPCQP_ERR_BAD_ARG;
+    if (B == 0) return MPCQP_OK;
+    hipSetDevice(c->device);
+    if (c->fast) {
+        FastArgs a = fast_args(c, B);
+        a.AB = const_cast<double *>(AB);
+        a.x0 = x0;
+        a.xref = xref;
+        a.contact = contact;
+        a.U = U;
+        a.cost = cost;
+        a.status = status;
+        a.iters = iters;
+        tbegin(c, 1);
+        const int rc = launch(c->fk.cs, B, c->fk.cs_lds, c->stream, &a);
+        tend(c, 1);
+        return rc;
+    }
+    // generic: condense from the given [Ad | Bd] into scratch H, f, then solve
+    int rc = ensure_scratch_hf(c, B);
+    if (rc) return rc;
+    CondenseArgs a = batch_condense_args(c, B, x0, xref, nullptr, c->scratchH, c->scratchF);
+    a.ABin = AB;
+    const size_t lds = set_lds((const void *)k_condense,
+                               sizeof(double) * condense_lds_doubles(c->m.nx, c->m.nu, c->m.N));
+    hipLaunchKernelGGL(k_condense, dim3(B), dim3(64), lds, c->stream, a);
+    rc = hip_status(hipGetLastError());
+    if (rc) return rc;
+    return mpcqp_batch_solve_qp(c, B, c->scratchH, c->scratchF, contact, U, cost, status, iters);
 }
 
 int mpcqp_batch_solve(mpcqp_ctx *c, int B, const double *x0, const double *xref,
@@ -630,20 +829,17 @@ int mpcqp_batch_solve(mpcqp_ctx *c, int B, const double *x0, const double *xref,
     if (!c) return MPCQP_ERR_BAD_ARG;
     if (B <= 0) return B == 0 ? MPCQP_OK : MPCQP_ERR_BAD_ARG;
     hipSetDevice(c->device);
-    const size_t nV = (size_t)c->m.nu * c->m.N;
-    if (c->scratch_cap < (size_t)B) {
-        hipFree(c->scratchH);
-        hipFree(c->scratchF);
-        c->scratchH = c->scratchF = nullptr;
-        c->scratch_cap = 0;
-        if (hipMalloc(&c->scratchH, sizeof(double) * nV * nV * B) != hipSuccess ||
-            hipMalloc(&c->scratchF, sizeof(double) * nV * B) != hipSuccess)
-            return MPCQP_ERR_DEVICE;
-        c->scratch_cap = B;
+    const size_t ab = (size_t)c->m.nx * (c->m.nx + c->m.nu);
+    if (c->ab_cap < (size_t)B) {
+        hipFree(c->dAB);
+        c->dAB = nullptr;
+        c->ab_cap = 0;
+        if (hipMalloc(&c->dAB, sizeof(double) * ab * B) != hipSuccess) return MPCQP_ERR_DEVICE;
+        c->ab_cap = B;
     }
-    int rc = mpcqp_batch_condense(c, B, x0, xref, lin, c->scratchH, c->scratchF);
+    int rc = mpcqp_batch_discretize(c, B, lin, c->dAB);
     if (rc) return rc;
-    return mpcqp_batch_solve_qp(c, B, c->scratchH, c->scratchF, contact, U, cost, status, iters);
+    return mpcqp_batch_condense_solve(c, B, c->dAB, x0, xref, contact, U, cost, status, iters);
 }
 
 int mpcqp_batch_select_min(mpcqp_ctx *c, int B, const double *cost, const int *status,

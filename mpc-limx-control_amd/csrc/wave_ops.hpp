@@ -53,9 +53,14 @@ __device__ __forceinline__ void wave_argmax(double &v, int &idx) {
     }
 }
 
-// Compiler + LDS ordering point between phases of a single-wave workgroup.  With a 64-thread
-// workgroup the backend drops the s_barrier itself; the workgroup fence keeps LDS stores of
-// one lane ordered before loads of another.
-__device__ __forceinline__ void wave_sync() { __syncthreads(); }
+// Ordering point between phases of a single-wave workgroup.  One wave issues its LDS
+// instructions in program order and the LDS executes them in order, so a store by one lane
+// is seen by a later load of another lane without any wait; only the compiler must not move
+// LDS accesses across this point (wavefront-scope fences emit no instruction).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 }  // namespace mpcqp

@@ -23,6 +23,7 @@ EXPORTS = [
     "mpcqp_discretize", "mpcqp_build_qp", "mpcqp_solve_dense", "mpcqp_plant_step",
     "mpcqp_ctx_create", "mpcqp_ctx_destroy", "mpcqp_set_stream", "mpcqp_sync",
     "mpcqp_batch_condense", "mpcqp_batch_solve_qp", "mpcqp_batch_solve",
+    "mpcqp_ctx_fast_path", "mpcqp_batch_discretize", "mpcqp_batch_condense_solve",
     "mpcqp_batch_select_min", "mpcqp_enable_timing", "mpcqp_last_kernel_ms",
     "mpcqp_status_string", "mpcqp_device_count",
 ]
@@ -69,6 +70,9 @@ def lib():
     L.mpcqp_batch_condense.argtypes = [vp, i, vp, vp, vp, vp, vp]
     L.mpcqp_batch_solve_qp.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp]
     L.mpcqp_batch_solve.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.mpcqp_ctx_fast_path.argtypes = [vp]
+    L.mpcqp_batch_discretize.argtypes = [vp, i, vp, vp]
+    L.mpcqp_batch_condense_solve.argtypes = [vp, i] + [vp] * 8
     L.mpcqp_batch_select_min.argtypes = [vp, i, vp, vp, C.c_int64, vp]
     L.mpcqp_enable_timing.argtypes = [vp, i]
     L.mpcqp_last_kernel_ms.argtypes = [vp, i]

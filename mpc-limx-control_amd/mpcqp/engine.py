@@ -80,6 +80,26 @@ class BatchEngine:
             self.ctx, d["B"], _ptr(H), _ptr(f), _ptr(d["contact"]), _ptr(d["U"]),
             _ptr(d["cost"]), _ptr(d["status"]), _ptr(d["iters"])))
 
+    @property
+    def fast_path(self) -> bool:
+        return bool(lib().mpcqp_ctx_fast_path(self.ctx))
+
+    def discretize(self, d, AB=None):
+        """stage 1: linearise + exp(M Ts) -> [Ad | Bd] per instance"""
+        t = self.torch
+        if AB is None:
+            nx, nu = self.p["nx"], self.p["nu"]
+            AB = t.empty((d["B"], nx * (nx + nu)), dtype=t.float64, device=d["x0"].device)
+        check("mpcqp_batch_discretize", lib().mpcqp_batch_discretize(
+            self.ctx, d["B"], _ptr(d["lin"]), _ptr(AB)))
+        return AB
+
+    def condense_solve(self, d, AB):
+        """stage 2: Phi, H_FF, f and the QP solve fused on chip"""
+        check("mpcqp_batch_condense_solve", lib().mpcqp_batch_condense_solve(
+            self.ctx, d["B"], _ptr(AB), _ptr(d["x0"]), _ptr(d["xref"]), _ptr(d["contact"]),
+            _ptr(d["U"]), _ptr(d["cost"]), _ptr(d["status"]), _ptr(d["iters"])))
+
     def solve(self, d):
         """linearise + discretise + condense + solve, all on device (async on the ctx stream)"""
         check("mpcqp_batch_solve", lib().mpcqp_batch_solve(

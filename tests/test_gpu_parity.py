@@ -105,9 +105,12 @@ def test_qpsolver_class_closed_loop(gpu, golden):
 
 
 # ------------------------------------------------------------------------- batched engine
-def run_batch(p, batch, want_hf=False):
+def run_batch(p, batch, want_hf=False, expect_fast=True):
+    """fused fast path (discretize + condense_solve); with want_hf also the generic path
+    (full H, f to HBM + stand-alone solve), whose results are returned under 'gen_*'."""
     from mpcqp.engine import BatchEngine
     eng = BatchEngine(p)
+    assert eng.fast_path == expect_fast
     d = eng.upload(batch)
     out = {}
     if want_hf:
@@ -116,9 +119,10 @@ def run_batch(p, batch, want_hf=False):
         eng.sync()
         out["H"] = H.cpu().numpy().transpose(0, 2, 1)  # stored column-major per instance
         out["f"] = f.cpu().numpy()
-    else:
-        eng.solve(d)
-        eng.sync()
+        for k in ("U", "cost", "status", "iters"):
+            out["gen_" + k] = d[k].cpu().numpy().copy()
+    eng.solve(d)
+    eng.sync()
     for k in ("U", "cost", "status", "iters"):
         out[k] = d[k].cpu().numpy()
     eng.close()
@@ -132,7 +136,9 @@ def test_batch_vs_golden(gpu, golden, fname):
     p = mpcqp.model_params(str(g["config"]))
     batch = dict(x0=g["x0"], xref=g["xref"], lin=g["lin"], contact=g["contact"])
     o = run_batch(p, batch, want_hf=True)
-    assert np.all(o["status"] == 0)
+    assert np.all(o["status"] == 0) and np.all(o["gen_status"] == 0)
+    for i in range(g["f"].shape[0]):
+        assert u_close(o["gen_U"][i], g["U"][i]), i
     for i in range(g["H"].shape[0]):
         assert rel_err(o["H"][i], g["H"][i]) <= TOL_COND
     for i in range(g["f"].shape[0]):
@@ -150,7 +156,10 @@ def test_batch_vs_oracle(gpu, orc, config, B):
     ref = orc.srbm_batch(p, batch["x0"], batch["xref"], batch["lin"], batch["contact"],
                          want_hf=True)
     np.testing.assert_array_equal(o["status"], ref["status"])
+    np.testing.assert_array_equal(o["gen_status"], ref["status"])
     assert np.all(o["status"] == 0)
+    bad_g = [i for i in range(B) if not u_close(o["gen_U"][i], ref["U"][i])]
+    assert not bad_g, bad_g[:10]
     for i in range(0, B, max(1, B // 64)):
         assert rel_err(o["H"][i], ref["H"][i]) <= TOL_COND
         assert rel_err(o["f"][i], ref["f"][i]) <= TOL_COND
@@ -223,6 +232,7 @@ def test_edge_cases(gpu):
     st, x, *_ = solve_dense(H, f, np.array([[1.0, 1.0, 0.0]]), None, None, np.array([1.0]),
                             np.array([1.0]))
     assert st == 0 and x[0] + x[1] == pytest.approx(1.0, abs=1e-12)
+    # a non-diagonal Q runs the generic kernels (same answers, see test_generic_path_*)
     # more free variables than the batched context was sized for -> BAD_DIMS per instance
     p2 = mpcqp.model_params("B")
     p2["max_free"] = 12
@@ -233,3 +243,20 @@ def test_edge_cases(gpu):
     eng.sync()
     assert np.all(d["status"].cpu().numpy() == 1)
     eng.close()
+
+
+def test_generic_path_non_diagonal_weights(gpu, orc):
+    """a full (non-diagonal) Q takes the generic runtime-dimension kernels; results still
+    match the oracle"""
+    import mpcqp
+    p = mpcqp.model_params("B")
+    rng = np.random.default_rng(3)
+    M = rng.normal(size=(13, 13)) * 0.05
+    p["Q"] = p["Q"] + M @ M.T
+    p["P"] = 20.0 * p["Q"]
+    batch = mpcqp.make_batch(p, 128, seed=5)
+    o = run_batch(p, batch, expect_fast=False)
+    ref = orc.srbm_batch(p, batch["x0"], batch["xref"], batch["lin"], batch["contact"])
+    assert np.all(o["status"] == 0)
+    for i in range(128):
+        assert u_close(o["U"][i], ref["U"][i]), i
