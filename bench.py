@@ -4,9 +4,9 @@ metric), batch 65,536 per GPU, 1..8 MI355X (one process per GPU, weak scaling: c
 524,288 = 65,536 x 8).
 
 One step = one pass of the hot path over the whole per-GPU batch, inputs resident in HBM:
-  k_condense (linearise + exp(M Ts) + Ad^k Bd + H, f) -> k_solve (Goldfarb-Idnani QP) ->
-  k_select_min (min-cost key) -> [N>1] RCCL MIN all-reduce of the 8-byte key + broadcast of
-  the winner's U (480 B).
+  k_mpc (linearise + discretise + condense + Goldfarb-Idnani solve, fused, one QP per
+  wavefront) -> k_select_min (min-cost key) -> [N>1] RCCL MIN all-reduce of the 8-byte key
+  + broadcast of the winner's U (480 B).
 
 Prints ONE JSON line on rank 0 (driver contract).
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config B|C|L]
@@ -101,12 +101,10 @@ def main():
     eng = BatchEngine(p, device=local)
     d = eng.upload(batch)
     nV = eng.nV
-    AB = eng.discretize(d)  # stage-1 output buffer, [B][nx*(nx+nu)]
     ubest = torch.zeros(nV, dtype=torch.float64, device=f"cuda:{local}")
 
     def step():
-        eng.discretize(d, AB)
-        eng.condense_solve(d, AB)
+        eng.solve(d)
         key = eng.select_min(d, index_base=rank * B)
         if world > 1:
             dist.all_reduce(key, op=dist.ReduceOp.MIN)
@@ -128,9 +126,8 @@ def main():
     for s in range(args.steps):
         e = ev[s]
         e[0].record(stream)
-        eng.discretize(d, AB)
+        eng.solve(d)
         e[1].record(stream)
-        eng.condense_solve(d, AB)
         e[2].record(stream)
         key = eng.select_min(d, index_base=rank * B)
         e[3].record(stream)
@@ -150,8 +147,8 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    disc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
-    cs_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    mpc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
+    sel_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
     status = d["status"].cpu().numpy()
     iters = d["iters"].cpu().numpy()
     solved = float(np.mean(status == 0))
@@ -160,13 +157,9 @@ def main():
         ms_per_step = elapsed / args.steps * 1e3
         total = B * world
         fl = algorithmic_flops(p["nx"], p["nu"], p["N"])
-        f_disc = fl["disc"] * B
-        f_cs = (fl["condense"] - fl["disc"] + fl["solve_fixed"] +
-                fl["per_iter"] * float(iters.mean())) * B
-        dom = "condense_solve" if cs_ms >= disc_ms else "discretize"
-        dom_ms = max(cs_ms, disc_ms)
-        dom_flops = f_cs if dom == "condense_solve" else f_disc
-        achieved = dom_flops / (dom_ms * 1e-3) / 1e12
+        f_qp = fl["condense"] + fl["solve_fixed"] + fl["per_iter"] * float(iters.mean())
+        dom_flops = f_qp * B
+        achieved = dom_flops / (mpc_ms * 1e-3) / 1e12
         out = dict(
             metric="QP solves/sec, 13-state N=10 SRBM MPC, batch=65536 at 1/2/4/8 MI355X",
             value=total / (elapsed / args.steps), unit="QP/s", n_gpus=world, steps=args.steps,
@@ -180,12 +173,12 @@ def main():
                         nu=p["nu"], config=args.config, parallelism=f"dp{world}",
                         solved_frac=solved, mean_solver_iters=float(iters.mean()),
                         fast_path=eng.fast_path,
-                        kernel_ms=dict(discretize=disc_ms, condense_solve=cs_ms)),
-            roofline=dict(bound="mfma", kernel=f"k_{dom}", achieved=achieved,
+                        kernel_ms=dict(k_mpc=mpc_ms, k_select_min=sel_ms)),
+            roofline=dict(bound="mfma", kernel="k_mpc", achieved=achieved,
                           peak=FP64_PEAK_TFLOPS, unit="TFLOP/s",
                           frac=achieved / FP64_PEAK_TFLOPS, traffic=None,
-                          algorithmic_flops_per_qp=dom_flops / B,
-                          whole_step_tflops=(f_disc + f_cs) / (ms_per_step * 1e-3) / 1e12),
+                          algorithmic_flops_per_qp=f_qp,
+                          whole_step_tflops=dom_flops / (ms_per_step * 1e-3) / 1e12),
         )
         if not args.no_cpu_baseline:
             cb, _ = cpu_baseline(p, batch)

@@ -165,6 +165,13 @@ int mpcqp_batch_select_min(mpcqp_ctx *ctx, int B, const double *cost, const int 
 int mpcqp_enable_timing(mpcqp_ctx *ctx, int on);
 double mpcqp_last_kernel_ms(mpcqp_ctx *ctx, int which);
 
+/* Diagnostics: per-phase cycle totals (s_memtime) of the fused kernels since the last call,
+ * recorded only by the diagnostic build lib/libmpcqp_stamps.so (first call arms it); the
+ * product library returns MPCQP_ERR_BAD_ARG.  Slots: 0 setup, 1 Phi/xf chains, 2 Qe,
+ * 3 H_FF, 4 gradient, 5 Cholesky, 6 J = L^-T, 7 unconstrained min, 8 dual loop, 9 write,
+ * 10 model build, 11 expm. */
+int mpcqp_debug_phase_cycles(mpcqp_ctx *ctx, uint64_t *out, int n);
+
 const char *mpcqp_status_string(int status);
 int mpcqp_device_count(void);
 

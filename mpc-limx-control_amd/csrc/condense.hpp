@@ -74,7 +74,7 @@ __device__ __forceinline__ double literal_entry(int i, int j, const double *lin,
 }
 
 // Fill T = [Ac | Bc] * Ts (nx x ns, column-major, ld nx) for this instance.
-__device__ inline void wave_build_model(const ModelConst &mc, const double *lin,
+__device__ __forceinline__ void wave_build_model(const ModelConst &mc, const double *lin,
                                         const double *Ac, const double *Bc, double *T) {
     const int nx = mc.nx, ns = mc.ns;
     double Iwi[9];
@@ -115,7 +115,7 @@ __device__ inline void wave_build_model(const ModelConst &mc, const double *lin,
 }
 
 // out = X * Y in the (top block, scalar) algebra: out[:,j] = X1 Y[:,j] (+ sY X[:,j] for j>=nx)
-__device__ inline void alg_mul(int nx, int ns, const double *X, const double *Y, double sY,
+__device__ __forceinline__ void alg_mul(int nx, int ns, const double *X, const double *Y, double sY,
                                double *out) {
     for (int e = lane(); e < nx * ns; e += kWave) {
         const int i = e % nx, j = e / nx;
@@ -129,7 +129,7 @@ __device__ inline void alg_mul(int nx, int ns, const double *X, const double *Y,
 
 // out = sum_q c[q] M[q] + cI * I (top block; diagonal of the top-left part)
 template <int K>
-__device__ inline void alg_comb(int nx, int ns, double *out, const double (&c)[K],
+__device__ __forceinline__ void alg_comb(int nx, int ns, double *out, const double (&c)[K],
                                 const double *const (&M)[K], double cI) {
     for (int e = lane(); e < nx * ns; e += kWave) {
         double s = 0.0;
@@ -144,7 +144,7 @@ __device__ inline void alg_comb(int nx, int ns, double *out, const double (&c)[K
 
 // E = exp([[A, B],[0, 0]]) top block, A = T (nx x ns, already scaled by Ts), Eigen's degree
 // selection.  ws: 7 * nx * ns doubles of scratch.  Result written to E (nx x ns).
-__device__ inline void wave_expm(int nx, int ns, double *T, double *ws, double *E) {
+__device__ __forceinline__ void wave_expm(int nx, int ns, double *T, double *ws, double *E) {
     const int sz = nx * ns;
     double *A2 = ws, *A4 = ws + sz, *A6 = ws + 2 * sz, *A8 = ws + 3 * sz, *U = ws + 4 * sz,
            *V = ws + 5 * sz, *W = ws + 6 * sz;
@@ -285,7 +285,7 @@ __device__ inline void wave_expm(int nx, int ns, double *T, double *ws, double *
 //   Phi, QPhi, PPhi: 3 * nx * nV   +   xf: nx * (N+1)   +   Qe: nx * (N+1).
 // Writes H (nV x nV column-major, global) and f (nV, global).  If xf_out != nullptr the
 // free response Ad^m x0 (m = 0..N) stays in ws for the caller (pointer returned there).
-__device__ inline void wave_condense(const ModelConst &mc, const double *AB, const double *x0,
+__device__ __forceinline__ void wave_condense(const ModelConst &mc, const double *AB, const double *x0,
                                      const double *xref, double *ws, double *H, double *f,
                                      double **Phi_out, double **xf_out) {
     const int nx = mc.nx, nu = mc.nu, N = mc.N, nV = mc.nV;

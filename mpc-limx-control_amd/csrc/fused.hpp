@@ -38,6 +38,7 @@ struct FastArgs {
     double *AB;                               // [B][NX*NS]
     double *U, *cost;
     int *status, *iters;
+    unsigned long long *stamps;               // diagnostic build only
 };
 
 template <int NX, int NU>
@@ -47,7 +48,7 @@ __host__ __device__ constexpr int disc_lds_doubles() {
 
 // ------------------------------------------------------------------ k_discretize
 template <int NX, int NU, int MODEL>
-__device__ inline void fast_discretize(const FastArgs &a, double *smem) {
+__device__ __forceinline__ void fast_discretize(const FastArgs &a, double *smem) {
     constexpr int NS = NX + NU;
     const int b = blockIdx.x;
     ModelConst mc;
@@ -60,8 +61,11 @@ __device__ inline void fast_discretize(const FastArgs &a, double *smem) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) lin[i] = a.lin[(size_t)b * 8 + i];
     double *T = smem, *ws = smem + NX * NS, *E = smem + 8 * NX * NS;
+    MPCQP_STAMP_INIT(tst);
     wave_build_model(mc, lin, nullptr, nullptr, T);
+    MPCQP_STAMP(a.stamps, 10, tst);
     wave_expm(NX, NS, T, ws, E);
+    MPCQP_STAMP(a.stamps, 11, tst);
     double *out = a.AB + (size_t)b * NX * NS;
     for (int e = lane(); e < NX * NS; e += kWave) out[e] = E[e];
 }
@@ -96,7 +100,7 @@ struct CSLayout {
 };
 
 template <int NX, int NU, int N, int MODEL, bool FRIC, int NFMAX>
-__device__ inline void fast_condense_solve(const FastArgs &a, unsigned char *smem) {
+__device__ __forceinline__ void fast_condense_solve(const FastArgs &a, unsigned char *smem) {
     using Lay = CSLayout<NX, NU, N, FRIC, NFMAX>;
     constexpr int NS = Lay::NS, NV = Lay::NV, LD = Lay::LD;
     const int b = blockIdx.x, ln = lane();
@@ -117,7 +121,9 @@ __device__ inline void fast_condense_solve(const FastArgs &a, unsigned char *sme
     P.mu = a.mu;
     P.mA = 0; P.A = nullptr; P.a_colmajor = 0; P.lbA = nullptr; P.ubA = nullptr;
     P.max_iter = a.max_iter;
+    MPCQP_STAMP_INIT(tst);
     GiCtx C;
+    C.stamps = a.stamps;
     C.P = &P;
     C.nfmax = NFMAX;
     C.L.ld = LD;
@@ -140,6 +146,7 @@ __device__ inline void fast_condense_solve(const FastArgs &a, unsigned char *sme
     gi_setup(C);  // free map + constraint states (independent of AB)
     if (C.nf > a.max_free) C.status = ST_BAD_DIMS;
     wave_sync();
+    MPCQP_STAMP(a.stamps, 0, tst);
     const double *Ad = AB, *Bd = AB + NX * NX;
 
     // ---- Phi_m = Ad Phi_{m-1} (Phi_0 = Bd) and free response xf_m = Ad xf_{m-1}
@@ -160,6 +167,7 @@ __device__ inline void fast_condense_solve(const FastArgs &a, unsigned char *sme
         }
         wave_sync();
     }
+    MPCQP_STAMP(a.stamps, 1, tst);
     // ---- weighted tracking errors Qe_m = W_m (xf_m - xref_m), m = 1..N
     const double *xr = a.xref + (size_t)b * NX * (N + 1);
     for (int e = ln; e < NX * N; e += kWave) {
@@ -169,6 +177,7 @@ __device__ inline void fast_condense_solve(const FastArgs &a, unsigned char *sme
     }
     wave_sync();
 
+    MPCQP_STAMP(a.stamps, 2, tst);
     const int nf = C.nf;
     if (C.status == ST_OK && nf > 0) {
         // ---- H_FF lower triangle, (p >= q) packed index e
@@ -194,6 +203,7 @@ __device__ inline void fast_condense_solve(const FastArgs &a, unsigned char *sme
             if (ki == kj) s += a.rmat[cj * NU + ci];
             C.L.R[q * LD + p] = 2.0 * s;
         }
+        MPCQP_STAMP(a.stamps, 3, tst);
         // ---- gradient of the free variables (fixed ones sit at 0 in this model)
         for (int p = ln; p < nf; p += kWave) {
             const int vi = C.L.fid[p], ki = vi / NU, ci = vi % NU;
@@ -210,7 +220,9 @@ __device__ inline void fast_condense_solve(const FastArgs &a, unsigned char *sme
     }
     C.c0 = 0.0;
     wave_sync();
+    MPCQP_STAMP(a.stamps, 4, tst);
     gi_run(C);
+    MPCQP_STAMP_INIT(tw);
     SolveOut O;
     O.x = a.U + (size_t)b * NV;
     O.cost = a.cost + b;
@@ -218,6 +230,7 @@ __device__ inline void fast_condense_solve(const FastArgs &a, unsigned char *sme
     O.iters = a.iters + b;
     O.y = nullptr;
     gi_write(C, O);
+    MPCQP_STAMP(a.stamps, 9, tw);
 }
 
 }  // namespace mpcqp

@@ -1,0 +1,285 @@
+// gi_reg.hpp -- register-resident Goldfarb-Idnani solve for up to NF <= 32 free variables.
+//
+// Same algorithm, constraint order and tolerances as gi_run (gi_solver.hpp) and the CPU
+// oracle; only the storage differs:
+//   * lane i holds row i of H_FF, then of L (Cholesky, right-looking, in place) -- h[NF]
+//   * lane c computes column c of L^-1 by forward substitution; since J = L^-T, that column
+//     is row c of J, which lane c keeps in registers -- Jr[NF]
+//   * lane 63 runs the same recurrence on g, yielding t = L^-1 g for free; then the
+//     unconstrained minimum is x = -J t and its objective -|t|^2 / 2
+//   * R stays in LDS (column-major, odd ld), as do x (xs) and the constraint states
+// All loops over columns are unrolled to NF with wave-uniform predicates, so every register
+// index is a compile-time constant (no scratch), and cross-lane reads are v_readlane with
+// constant lane indices.
+#pragma once
+#include "gi_solver.hpp"
+
+namespace mpcqp {
+
+// Row-broadcast of J: d_j = sum over the (<= 2) nonzero entries of n_p of n_a * J(a, j).
+template <int NF>
+__device__ __forceinline__ double reg_project(const double (&Jr)[NF], int a0, double c0,
+                                              int a1, double c1, double *rowbuf) {
+    const int ln = lane();
+    // lane a0 (and a1) publish their rows scaled by the normal's coefficients
+    if (ln == a0) {
+#pragma unroll
+        for (int c = 0; c < NF; ++c) rowbuf[c] = c0 * Jr[c];
+    }
+    wave_sync();
+    if (a1 >= 0 && ln == a1) {
+#pragma unroll
+        for (int c = 0; c < NF; ++c) rowbuf[c] += c1 * Jr[c];
+    }
+    wave_sync();
+    const double d = (ln < NF) ? rowbuf[ln] : 0.0;
+    wave_sync();
+    return d;
+}
+
+template <int NF>
+__device__ __forceinline__ void gi_project_reg(const GiCtx &C, const double (&Jr)[NF], int id, double x,
+                                      double &dj, double &sp, double *rowbuf) {
+    const SolveProblem &P = *C.P;
+    const GiLds &L = C.L;
+    const int nf = C.nf, nfric = C.nfric, ln = lane();
+    const double b = gi_cons_b(C, id);
+    if (id < 2 * nf) {
+        const int a = id < nf ? id : id - nf;
+        const double sg = id < nf ? 1.0 : -1.0;
+        dj = reg_project<NF>(Jr, a, sg, -1, 0.0, rowbuf);
+        sp = sg * readlane(x, a) - b;
+    } else {
+        // friction row (the fast path has no dense rows)
+        const int r = id - 2 * nf, ks = r >> 2, t = r & 3;
+        const int k = ks / P.nfeet, sft = ks % P.nfeet;
+        const int pz = L.pos[k * P.nu + 3 * sft + 2], pt = L.pos[k * P.nu + 3 * sft + (t >> 1)];
+        const double sg = (t & 1) ? 1.0 : -1.0;
+        double nx_ = 0.0;
+        if (pz >= 0 && pt >= 0) {
+            dj = reg_project<NF>(Jr, pz, P.mu, pt, sg, rowbuf);
+            nx_ = P.mu * readlane(x, pz) + sg * readlane(x, pt);
+        } else if (pz >= 0) {
+            dj = reg_project<NF>(Jr, pz, P.mu, -1, 0.0, rowbuf);
+            nx_ = P.mu * readlane(x, pz);
+        } else {
+            dj = reg_project<NF>(Jr, pt, sg, -1, 0.0, rowbuf);
+            nx_ = sg * readlane(x, pt);
+        }
+        sp = nx_ - b;
+    }
+    (void)nfric;
+    if (ln >= nf) dj = 0.0;
+}
+
+// h: lane p holds row p of H_FF (columns < nf meaningful), g: lane p holds g_p.
+// rowbuf: NF doubles of LDS.  Fills C.{status,x,u,fval,act,q,iters}.
+template <int NF>
+__device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, double *rowbuf) {
+    static_assert(NF <= 32, "register path holds at most 32 free variables");
+    GiLds &L = C.L;
+    const SolveProblem &P = *C.P;
+    const int nf = C.nf, ld = L.ld, ln = lane(), mt = C.mt;
+    int status = C.status;
+    double fval = 0.0, x = 0.0, u = 0.0;
+    int iters = 0, q = 0, act = -1;
+    double Jr[NF];
+    MPCQP_STAMP_INIT(tst);
+
+    if (status == ST_OK && nf > 0) {
+        // ---- Cholesky, right-looking; lane i owns row i.  h is padded with the identity
+        //      beyond nf, so every step runs unpredicated (upper-triangle junk is never read)
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < NF; ++k) {
+            const double piv = readlane(h[k], k);
+            bad |= !(piv > 0.0);
+            const double lkk = sqrt(piv);
+            const double lik = (ln == k) ? lkk : h[k] / lkk;
+            h[k] = lik;
+#pragma unroll
+            for (int j = 0; j < NF; ++j)
+                if (j > k) h[j] -= lik * readlane(lik, j);
+#pragma unroll
+            for (int j = 0; j < NF; ++j)
+                if (j >= k) pin(h[j]);  // step k's updates happen in step k
+            step_fence();
+        }
+        if (bad) status = ST_NOT_PD;
+    }
+    MPCQP_STAMP(C.stamps, 5, tst);
+    if (status == ST_OK && nf > 0) {
+        // ---- park L in the (still empty) R buffer: lane i stores row i, L(i,l) at l*ld + i
+#pragma unroll
+        for (int l = 0; l < NF; ++l)
+            if (ln < NF && l <= ln) L.R[l * ld + ln] = h[l];
+        wave_sync();
+        // ---- columns of L^-1 (lane c), plus t = L^-1 g on lane 63; L(i,l) are uniform-
+        //      address LDS broadcasts, so only J occupies registers here
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            double s = (ln == 63) ? readlane(g, i) : ((ln == i) ? 1.0 : 0.0);
+#pragma unroll
+            for (int l = 0; l < NF; ++l) {
+                if (l < i) s -= L.R[l * ld + i] * Jr[l];
+            }
+            Jr[i] = s / L.R[i * ld + i];
+            pin(Jr[i]);
+            step_fence();  // keep step i's loads and arithmetic in step i
+        }
+        MPCQP_STAMP(C.stamps, 6, tst);
+        // ---- unconstrained minimum x = -J t, objective -|t|^2/2
+        double s = 0.0, tt = 0.0;
+#pragma unroll
+        for (int j = 0; j < NF; ++j) {
+            const double tj = readlane(Jr[j], 63);  // t_j = 0 beyond nf (g padded with 0)
+            s += Jr[j] * tj;
+            tt += tj * tj;
+        }
+        x = (ln < nf) ? -s : 0.0;
+        fval = -0.5 * tt;
+        // lanes nf..NF-1 keep their identity rows of J (decoupled from the free block);
+        // lanes >= NF (incl. lane 63) hold zeros
+        if (ln >= NF) {
+#pragma unroll
+            for (int j = 0; j < NF; ++j) Jr[j] = 0.0;
+        }
+        if (ln < nf) L.xs[ln] = x;
+        wave_sync();
+    }
+    MPCQP_STAMP(C.stamps, 7, tst);
+
+    const int max_iter = P.max_iter > 0 ? P.max_iter : 10 * (mt + nf + 1);
+    bool done = (status != ST_OK) || nf == 0;
+    while (!done) {
+        // ---- step 1: most violated inactive constraint (lowest id on ties)
+        double best = INFINITY;
+        int bid = 0x7fffffff;
+        for (int id = ln; id < mt; id += kWave) {
+            if (L.st[id] != 1) continue;
+            const double s = gi_cons_slack_lane(C, id);
+            if (s < -kFeasTol * (1.0 + fabs(gi_cons_b(C, id))) && s < best) { best = s; bid = id; }
+        }
+        wave_argmin(best, bid);
+        if (bid == 0x7fffffff) break;  // optimal
+        const int p = bid;
+        double dj, sp;
+        gi_project_reg<NF>(C, Jr, p, x, dj, sp, rowbuf);
+        if (ln == q) u = 0.0;
+        // ---- step 2
+        for (;;) {
+            if (iters >= max_iter) { status = ST_ITER_LIMIT; done = true; break; }
+            ++iters;
+            const double dd = wave_sum(ln < nf ? dj * dj : 0.0);
+            const double zn = wave_sum((ln >= q && ln < nf) ? dj * dj : 0.0);
+            double z = 0.0;
+#pragma unroll
+            for (int j = 0; j < NF; ++j)
+                if (j >= q) z += Jr[j] * readlane(dj, j);  // d_j = 0 for j >= nf
+            // r = R^-1 d(0:q) (R in LDS)
+            double r = 0.0, val = dj;
+            for (int j = q - 1; j >= 0; --j) {
+                const double rj = readlane(val, j) / L.R[j * ld + j];
+                if (ln == j) r = rj;
+                if (ln < j) val -= L.R[j * ld + ln] * rj;
+            }
+            const double rmax = wave_max(ln < q ? fabs(r) : 0.0);
+            double t1 = INFINITY;
+            int kslot = 0x7fffffff;
+            if (ln < q && r > kRTol * rmax) { t1 = u / r; kslot = ln; }
+            wave_argmin(t1, kslot);
+            const bool dep = !(zn > kDepTol * dd);
+            const double t2 = dep ? INFINITY : -sp / zn;
+            const double t = t1 < t2 ? t1 : t2;
+            if (isinf(t)) { status = ST_INFEASIBLE; done = true; break; }
+            const double uq = readlane(u, q);
+            if (isinf(t2)) {
+                if (ln < q) u -= t * r;
+                if (ln == q) u += t;
+            } else {
+                if (ln < nf) { x += t * z; L.xs[ln] = x; }
+                fval += t * zn * (0.5 * t + uq);
+                if (ln < q) u -= t * r;
+                if (ln == q) u += t;
+                if (t2 <= t1) {
+                    // ---- add p: Givens chain on d from the bottom up to q+1, applied to the
+                    //      J columns held in registers
+                    double acc = readlane(dj, nf - 1);
+#pragma unroll
+                    for (int j = NF - 1; j >= 1; --j) {
+                        if (j > q && j < nf) {
+                            const double a = readlane(dj, j - 1);
+                            double c = 1.0, s = 0.0, hh = a;
+                            if (acc != 0.0) {
+                                hh = sqrt(a * a + acc * acc);
+                                const double ih = 1.0 / hh;
+                                c = a * ih;
+                                s = acc * ih;
+                            }
+                            acc = hh;
+                            const double x0 = Jr[j - 1], x1 = Jr[j];
+                            Jr[j - 1] = c * x0 + s * x1;
+                            Jr[j] = -s * x0 + c * x1;
+                        }
+                    }
+                    const double rqq = (q < nf - 1) ? acc : readlane(dj, q);
+                    if (ln < q) L.R[q * ld + ln] = dj;
+                    if (ln == q) { L.R[q * ld + q] = rqq; act = p; }
+                    if (ln == 0) L.st[p] = 2;
+                    ++q;
+                    wave_sync();
+                    break;
+                }
+            }
+            // ---- drop slot kslot
+            const int k = kslot;
+            const int dropped = readlane(act, k);
+            if (ln == 0) L.st[dropped] = 1;
+            {
+                const int src = ln + 1 < kWave ? ln + 1 : ln;
+                const double un = __shfl(u, src, kWave);
+                const int an = __shfl(act, src, kWave);
+                if (ln >= k && ln < q) { u = un; act = an; }
+            }
+            for (int j = k; j < q - 1; ++j) {
+                const double v = (ln <= j + 1) ? L.R[(j + 1) * ld + ln] : 0.0;
+                wave_sync();
+                if (ln <= j + 1) L.R[j * ld + ln] = v;
+                wave_sync();
+            }
+            --q;
+#pragma unroll
+            for (int j = 0; j < NF - 1; ++j) {
+                if (j >= k && j < q) {
+                    const double a = L.R[j * ld + j], bb = L.R[j * ld + j + 1];
+                    if (bb != 0.0) {
+                        const double hh = sqrt(a * a + bb * bb);
+                        const double ih = 1.0 / hh;
+                        const double c = a * ih, s = bb * ih;
+                        const int l = j + 1 + ln;
+                        double r0 = 0.0, r1 = 0.0;
+                        if (l < q) { r0 = L.R[l * ld + j]; r1 = L.R[l * ld + j + 1]; }
+                        wave_sync();
+                        if (l < q) { L.R[l * ld + j] = c * r0 + s * r1; L.R[l * ld + j + 1] = -s * r0 + c * r1; }
+                        if (ln == 0) { L.R[j * ld + j] = hh; L.R[j * ld + j + 1] = 0.0; }
+                        wave_sync();
+                        const double x0 = Jr[j], x1 = Jr[j + 1];
+                        Jr[j] = c * x0 + s * x1;
+                        Jr[j + 1] = -s * x0 + c * x1;
+                    }
+                }
+            }
+            gi_project_reg<NF>(C, Jr, p, x, dj, sp, rowbuf);
+        }
+    }
+    MPCQP_STAMP(C.stamps, 8, tst);
+    C.status = status;
+    C.x = x;
+    C.u = u;
+    C.fval = fval;
+    C.act = act;
+    C.q = q;
+    C.iters = iters;
+}
+
+}  // namespace mpcqp

@@ -81,7 +81,7 @@ struct GiLds {
     int ld;
 };
 
-__device__ inline GiLds gi_carve(unsigned char *base, int nfmax, int nV, int mA) {
+__device__ __forceinline__ GiLds gi_carve(unsigned char *base, int nfmax, int nV, int mA) {
     GiLds L;
     L.ld = nfmax | 1;
     double *d = reinterpret_cast<double *>(base);
@@ -108,6 +108,7 @@ struct GiCtx {
     // results of gi_run
     double x, u, fval;
     int act, q, iters;
+    unsigned long long *stamps;  // diagnostic phase cycles (nullptr: off)
 };
 
 __device__ __forceinline__ double rowA(const SolveProblem &P, int r, int v) {
@@ -133,7 +134,7 @@ __device__ __forceinline__ void var_bounds(const SolveProblem &P, int v, double 
 
 // ---------------------------------------------------------------- constraint accessors
 // b of the one-sided constraint id (normal' x_F >= b, fixed parts folded into b)
-__device__ inline double gi_cons_b(const GiCtx &C, int id) {
+__device__ __forceinline__ double gi_cons_b(const GiCtx &C, int id) {
     const SolveProblem &P = *C.P;
     const GiLds &L = C.L;
     const int nf = C.nf, nfric = C.nfric;
@@ -155,7 +156,7 @@ __device__ inline double gi_cons_b(const GiCtx &C, int id) {
 }
 
 // slack n'x - b of constraint id evaluated by ONE lane (x read from the LDS mirror)
-__device__ inline double gi_cons_slack_lane(const GiCtx &C, int id) {
+__device__ __forceinline__ double gi_cons_slack_lane(const GiCtx &C, int id) {
     const SolveProblem &P = *C.P;
     const GiLds &L = C.L;
     const int nf = C.nf, nfric = C.nfric;
@@ -180,7 +181,7 @@ __device__ inline double gi_cons_slack_lane(const GiCtx &C, int id) {
 }
 
 // d_j = (J' n_p)_j on lane j, and the slack n_p'x - b (uniform); x: lane i holds x_i
-__device__ inline void gi_cons_project(const GiCtx &C, int id, double x, double &dj, double &sp) {
+__device__ __forceinline__ void gi_cons_project(const GiCtx &C, int id, double x, double &dj, double &sp) {
     const SolveProblem &P = *C.P;
     const GiLds &L = C.L;
     const int nf = C.nf, nfric = C.nfric, ld = L.ld, ln = lane();
@@ -216,7 +217,7 @@ __device__ inline void gi_cons_project(const GiCtx &C, int id, double x, double 
 
 // ---------------------------------------------------------------- stage 1: setup
 // Fixed variables, free index map, constraint states.  Leaves C.nf, C.mt, C.status.
-__device__ inline void gi_setup(GiCtx &C) {
+__device__ __forceinline__ void gi_setup(GiCtx &C) {
     const SolveProblem &P = *C.P;
     GiLds &L = C.L;
     const int nV = P.nV, mA = P.mA, ln = lane(), nfmax = C.nfmax;
@@ -298,7 +299,7 @@ __device__ inline void gi_setup(GiCtx &C) {
 
 // ---------------------------------------------------------------- stage 2: gather
 // H_FF (lower triangle suffices) into R, g = f_F + H_FB x_B, c0 = fixed-part objective.
-__device__ inline void gi_gather(GiCtx &C) {
+__device__ __forceinline__ void gi_gather(GiCtx &C) {
     const SolveProblem &P = *C.P;
     GiLds &L = C.L;
     const int nV = P.nV, nf = C.nf, ld = L.ld, ln = lane();
@@ -327,13 +328,14 @@ __device__ inline void gi_gather(GiCtx &C) {
 }
 
 // ---------------------------------------------------------------- stage 3: factor + loop
-__device__ inline void gi_run(GiCtx &C) {
+__device__ __forceinline__ void gi_run(GiCtx &C) {
     const SolveProblem &P = *C.P;
     GiLds &L = C.L;
     const int nf = C.nf, ld = L.ld, ln = lane(), mt = C.mt, nfric = C.nfric;
     double fval = 0.0, x = 0.0, u = 0.0;
     int iters = 0, q = 0, act = -1, eqs = 0;
     int status = C.status;
+    MPCQP_STAMP_INIT(tst);
 
     if (status == ST_OK && nf > 0) {
         // Cholesky H_FF = L L' in place (lower), left-looking by column
@@ -363,6 +365,7 @@ __device__ inline void gi_run(GiCtx &C) {
             }
         C.c0 = wave_sum(cl);
     }
+    MPCQP_STAMP(C.stamps, 5, tst);
 
     if (status == ST_OK && nf > 0) {
         // J = L^-T: lane c computes column c of L^-1 and stores Linv(i, c) at J[i*ld + c],
@@ -376,6 +379,7 @@ __device__ inline void gi_run(GiCtx &C) {
             }
         }
         wave_sync();
+        MPCQP_STAMP(C.stamps, 6, tst);
         // unconstrained minimum x = -J J' g
         double w = 0.0;
         if (ln < nf)
@@ -390,6 +394,7 @@ __device__ inline void gi_run(GiCtx &C) {
         if (ln < nf) L.xs[ln] = x;
         wave_sync();
     }
+    MPCQP_STAMP(C.stamps, 7, tst);
 
     const int max_iter = P.max_iter > 0 ? P.max_iter : 10 * (mt + nf + 1);
     int eq_next = 2 * nf + nfric;  // dense rows are the only equality candidates
@@ -535,6 +540,7 @@ __device__ inline void gi_run(GiCtx &C) {
             gi_cons_project(C, p, x, dj, sp);
         }
     }
+    MPCQP_STAMP(C.stamps, 8, tst);
     C.status = status;
     C.x = x;
     C.u = u;
@@ -545,7 +551,7 @@ __device__ inline void gi_run(GiCtx &C) {
 }
 
 // ---------------------------------------------------------------- stage 4: outputs
-__device__ inline void gi_write(GiCtx &C, const SolveOut &O) {
+__device__ __forceinline__ void gi_write(GiCtx &C, const SolveOut &O) {
     const SolveProblem &P = *C.P;
     GiLds &L = C.L;
     const int nV = P.nV, mA = P.mA, nf = C.nf, ln = lane(), nfric = C.nfric;
@@ -589,9 +595,10 @@ __device__ inline void gi_write(GiCtx &C, const SolveOut &O) {
 }
 
 // Stand-alone solve of one instance from H, f in global memory (LDS: gi_lds_bytes).
-__device__ inline void wave_gi_solve(const SolveProblem &P, const SolveOut &O,
+__device__ __forceinline__ void wave_gi_solve(const SolveProblem &P, const SolveOut &O,
                                      unsigned char *smem, int nfmax) {
     GiCtx C;
+    C.stamps = nullptr;
     C.P = &P;
     C.L = gi_carve(smem, nfmax, P.nV, P.mA);
     C.nfmax = nfmax;

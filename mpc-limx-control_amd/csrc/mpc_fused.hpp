@@ -1,0 +1,310 @@
+// mpc_fused.hpp -- one kernel for the whole per-tick step of the TRON1 models:
+// linearise -> discretise -> condense -> solve, one QP per wavefront, nothing but U / cost /
+// status / iterations leaving the chip.
+//
+// Reference: mpcQP::mpcQP + buildSystemModel (include/mpcQP.h:35-119, 121-182),
+// QPSolver::discretizeSystem / buildQPParams / solveQP (src/QPSolver.cpp:21-106).
+//
+// Closed-form discretisation and condensing.  For both TRON1 models (the convex-MPC SRBM and
+// the reference-literal 13x3) the continuous dynamics are nilpotent: with A = Ac Ts and
+// B = Bc Ts, A^2 has a single non-zero (p_z <- g) and A^3 = 0, and the gravity row of Bc is
+// zero so A^2 B = 0.  Hence, exactly,
+//   exp([[A, B],[0, 0]]) = I + M + M^2/2 + M^3/6:   Ad = I + A + A^2/2,   Bd = B + AB/2
+//   Ad^m = I + m A + m^2 A^2 / 2,     Phi_m = Ad^m Bd = B + (m + 1/2) A B.
+// Eigen's Pade approximant (what the reference evaluates) agrees with this series to beyond
+// the 4th power, so the two are equal in exact arithmetic; in fp64 they agree to ~1e-16
+// (tests/test_gpu_parity.py).  With Phi_a = X0 + beta_a X1 (X0 = B, X1 = AB, beta_a = a+1/2)
+// and diagonal weights W_m (Q for m < N, P for m = N):
+//   H(i,j)/2 = sum_m sum_rs beta_i^r beta_j^s S^{W_m}_rs(c_i,c_j) + R(c_i,c_j)[k_i == k_j],
+//   S^W_rs = X_r' W X_s  (eight 6x6 blocks, 13-deep),
+// and the sums over m of 1, beta_i, beta_j, beta_i beta_j have closed forms.
+//   f(i) = 2 sum_{m>k_i} (u_m(c_i) + beta_{m-1-k_i} v_m(c_i)),
+//   u_m = X0' W_m e_m, v_m = X1' W_m e_m, e_m = x0 + m A x0 + m^2 A^2 x0 / 2 - xref_m.
+#pragma once
+#include "condense.hpp"
+#include "gi_reg.hpp"
+#include "gi_solver.hpp"
+
+namespace mpcqp {
+
+struct MpcArgs {
+    int B;
+    double Ts, mass;
+    double Ibinv[9];
+    const double *qd, *pd;  // diagonals of Q and P (device)
+    const double *rmat;     // R, nu x nu column-major (device)
+    double fz_min, fz_max, fxy_max, u_min, u_max, mu;
+    int max_iter, max_free;
+    const double *lin, *x0, *xref;
+    const uint64_t *contact;
+    double *U, *cost;
+    int *status, *iters;
+    unsigned long long *stamps;
+};
+
+template <int NU, int N, bool FRIC, int NF>
+struct MpcLayout {
+    static constexpr int NX = 13, NV = NU * N, LD = NF | 1;
+    static constexpr int NFRIC = FRIC ? 4 * N * 2 : 0;
+    static constexpr int MT = 2 * NF + NFRIC;
+    static constexpr bool REG = NF <= 32;
+    // doubles
+    static constexpr int oX0 = 0;                        // B  (NX x NU)
+    static constexpr int oX1 = oX0 + NX * NU;            // AB (NX x NU)
+    static constexpr int oS = oX1 + NX * NU;             // S[w][r][s] (8 x NU x NU)
+    static constexpr int oUV = oS + 8 * NU * NU;         // u_m, v_m: [(N+1)][2][NU]
+    static constexpr int oAx = oUV + (N + 1) * 2 * NU;   // A x0 (NX), A^2 x0 (NX)
+    static constexpr int oR = oAx + 2 * NX;              // R factor (NF x LD)
+    static constexpr int oJ = oR + NF * LD;              // J (LDS solver only)
+    static constexpr int oRow = oJ + (REG ? 0 : NF * LD);// row broadcast buffer (NF)
+    static constexpr int oG = oRow + NF;                 // g (LDS solver)
+    static constexpr int oXS = oG + NF;
+    static constexpr int oXF = oXS + NF;                 // xfull (NV)
+    static constexpr int oMisc = oXF + NV;               // rowfix / ys slot
+    static constexpr int oXr = oMisc + 2;                // xref (NX x (N+1)) prefetch
+    static constexpr int oX0v = oXr + NX * (N + 1);      // x0 prefetch (NX)
+    static constexpr int nDoubles = oX0v + NX + 1;
+    static constexpr size_t bytes =
+        sizeof(double) * nDoubles + sizeof(int) * (NF + NV) + ((MT + 15) & ~15);
+    static constexpr size_t lds_bytes = (bytes + 15) & ~(size_t)15;
+};
+
+// sum over m in [m0, m1] of 1, beta_i, beta_j, beta_i beta_j; beta_x = m - 1 - k_x + 1/2
+__device__ __forceinline__ void beta_sums(int m0, int m1, int ki, int kj, double &c, double &si,
+                                          double &sj, double &sij) {
+    if (m1 < m0) { c = si = sj = sij = 0.0; return; }
+    const double n = (double)(m1 - m0 + 1);
+    const double s1 = 0.5 * (double)(m0 + m1) * n;  // sum m
+    auto S2 = [](int t) { return (double)t * (t + 1) * (2 * t + 1) / 6.0; };
+    const double s2 = S2(m1) - S2(m0 - 1);           // sum m^2
+    const double oi = (double)ki + 0.5, oj = (double)kj + 0.5;
+    c = n;
+    si = s1 - oi * n;
+    sj = s1 - oj * n;
+    sij = s2 - (oi + oj) * s1 + oi * oj * n;
+}
+
+template <int NU, int N, int MODEL, bool FRIC, int NF>
+__device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) {
+    using Lay = MpcLayout<NU, N, FRIC, NF>;
+    constexpr int NX = 13, NS = NX + NU, NV = Lay::NV, LD = Lay::LD;
+    const int b = blockIdx.x, ln = lane();
+    double *D = reinterpret_cast<double *>(smem);
+    double *X0 = D + Lay::oX0, *X1 = D + Lay::oX1, *S = D + Lay::oS, *UV = D + Lay::oUV;
+    double *Ax = D + Lay::oAx, *A2x = Ax + NX;
+    MPCQP_STAMP_INIT(tst);
+
+    // ---- solver context (bounds from the contact schedule)
+    SolveProblem P;
+    P.nV = NV;
+    P.H = nullptr; P.f = nullptr; P.lb = nullptr; P.ub = nullptr;
+    P.gen_bounds = 1;
+    P.model = MODEL; P.nu = NU; P.N = N; P.nfeet = 2;
+    P.fz_min = a.fz_min; P.fz_max = a.fz_max; P.fxy_max = a.fxy_max;
+    P.u_min = a.u_min; P.u_max = a.u_max;
+    P.contact = (MODEL == 0) ? a.contact[b] : 0ull;
+    P.friction = FRIC ? 1 : 0;
+    P.mu = a.mu;
+    P.mA = 0; P.A = nullptr; P.a_colmajor = 0; P.lbA = nullptr; P.ubA = nullptr;
+    P.max_iter = a.max_iter;
+    GiCtx C;
+    C.stamps = a.stamps;
+    C.P = &P;
+    C.nfmax = NF;
+    C.L.ld = LD;
+    C.L.R = D + Lay::oR;
+    C.L.J = D + Lay::oJ;
+    C.L.g = D + Lay::oG;
+    C.L.xs = D + Lay::oXS;
+    C.L.xfull = D + Lay::oXF;
+    C.L.rowfix = D + Lay::oMisc;
+    C.L.ys = D + Lay::oMisc;
+    int *ip = reinterpret_cast<int *>(D + Lay::nDoubles);
+    C.L.fid = ip;
+    C.L.pos = ip + NF;
+    C.L.st = reinterpret_cast<unsigned char *>(ip + NF + NV);
+
+    // ---- per-instance inputs: one coalesced sweep into LDS
+    double *xr = D + Lay::oXr, *x0g = D + Lay::oX0v;
+    {
+        const double *xrg = a.xref + (size_t)b * NX * (N + 1);
+        for (int e = ln; e < NX * (N + 1); e += kWave) xr[e] = xrg[e];
+        if (ln < NX) x0g[ln] = a.x0[(size_t)b * NX + ln];
+    }
+    // ---- model: X0 = Bc Ts, X1 = (Ac Ts)(Bc Ts); A x0, A^2 x0
+    double lin[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) lin[i] = a.lin[(size_t)b * 8 + i];
+    wave_sync();
+    double Iwi[9];
+    double cy = 1.0, sy = 0.0;
+    if (MODEL == 0) {
+        sincos(lin[0], &sy, &cy);
+        const double Rz[9] = {cy, sy, 0.0, -sy, cy, 0.0, 0.0, 0.0, 1.0};
+        double Tm[9];
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                double s = 0.0;
+#pragma unroll
+                for (int l = 0; l < 3; ++l) s += Rz[l * 3 + i] * a.Ibinv[j * 3 + l];
+                Tm[j * 3 + i] = s;
+            }
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                double s = 0.0;
+#pragma unroll
+                for (int l = 0; l < 3; ++l) s += Tm[l * 3 + i] * Rz[l * 3 + j];
+                Iwi[j * 3 + i] = s;
+            }
+    }
+    auto entry = [&](int i, int j) -> double {  // [Ac | Bc](i, j)
+        return MODEL == 0 ? srbm_entry(i, j, lin, cy, sy, Iwi, a.mass)
+                          : literal_entry(i, j, lin, a.mass);
+    };
+    const double Ts = a.Ts;
+    for (int e = ln; e < NX * NU; e += kWave) {
+        const int i = e % NX, c = e / NX;
+        X0[e] = entry(i, NX + c) * Ts;
+    }
+    if (ln < NX) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < NX; ++k) s += entry(ln, k) * x0g[k];
+        Ax[ln] = s * Ts;
+    }
+    wave_sync();
+    for (int e = ln; e < NX * NU; e += kWave) {
+        const int i = e % NX, c = e / NX;
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < NX; ++k) s += entry(i, k) * X0[c * NX + k];
+        X1[e] = s * Ts;
+    }
+    if (ln < NX) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < NX; ++k) s += entry(ln, k) * Ax[k];
+        A2x[ln] = s * Ts;
+    }
+    gi_setup(C);  // free map + constraint states
+    if (C.nf > a.max_free) C.status = ST_BAD_DIMS;
+    wave_sync();
+    MPCQP_STAMP(a.stamps, 0, tst);
+
+    // ---- S^W_rs = X_r' W X_s   (w: 0 = Q, 1 = P), stored [w][r][s][cj][ci]; the block
+    //      loop is wave-uniform so the weights are scalar loads
+#pragma unroll
+    for (int rs = 0; rs < 8; ++rs) {
+        const int s_ = rs & 1, r_ = (rs >> 1) & 1, w_ = rs >> 2;
+        const double *Xr = r_ ? X1 : X0, *Xs = s_ ? X1 : X0;
+        const double *w = w_ ? a.pd : a.qd;
+        for (int e = ln; e < NU * NU; e += kWave) {
+            const int ci = e % NU, cj = e / NU;
+            double acc = 0.0;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) acc += Xr[ci * NX + l] * w[l] * Xs[cj * NX + l];
+            S[rs * NU * NU + e] = acc;
+        }
+    }
+    // ---- u_m(c) = X0[:,c]' W_m e_m, v_m(c) = X1[:,c]' W_m e_m, m = 1..N
+    for (int e = ln; e < N * NU; e += kWave) {
+        const int c = e % NU, m = 1 + e / NU;
+        const double md = (double)m, hm2 = 0.5 * md * md;
+        double su = 0.0, sv = 0.0;
+#pragma unroll
+        for (int l = 0; l < NX; ++l) {
+            const double wl = (m < N) ? a.qd[l] : a.pd[l];
+            const double el = wl * (x0g[l] + md * Ax[l] + hm2 * A2x[l] - xr[m * NX + l]);
+            su += X0[c * NX + l] * el;
+            sv += X1[c * NX + l] * el;
+        }
+        UV[(m * 2 + 0) * NU + c] = su;
+        UV[(m * 2 + 1) * NU + c] = sv;
+    }
+    wave_sync();
+    MPCQP_STAMP(a.stamps, 1, tst);
+
+    // ---- H_FF (lane p builds row p) and g
+    const int nf = C.nf;
+    const bool ok = C.status == ST_OK && nf > 0;
+    auto H_entry = [&](int vi, int vj) -> double {
+        const int ki = vi / NU, ci = vi % NU, kj = vj / NU, cj = vj % NU;
+        const int kk = ki > kj ? ki : kj;
+        double c, si, sj, sij;
+        beta_sums(kk + 1, N - 1, ki, kj, c, si, sj, sij);
+        const double bi = (double)(N - 1 - ki) + 0.5, bj = (double)(N - 1 - kj) + 0.5;
+        const int o = cj * NU + ci, nn = NU * NU;
+        double v = c * S[0 * nn + o] + sj * S[1 * nn + o] + si * S[2 * nn + o] + sij * S[3 * nn + o];
+        v += S[4 * nn + o] + bj * S[5 * nn + o] + bi * S[6 * nn + o] + bi * bj * S[7 * nn + o];
+        if (ki == kj) v += a.rmat[cj * NU + ci];
+        return 2.0 * v;
+    };
+    double gp = 0.0;
+    if (ok && ln < nf) {
+        const int vi = C.L.fid[ln], ki = vi / NU, ci = vi % NU;
+        double s = 0.0;
+        for (int m = ki + 1; m <= N; ++m) {
+            const double beta = (double)(m - 1 - ki) + 0.5;
+            s += UV[(m * 2 + 0) * NU + ci] + beta * UV[(m * 2 + 1) * NU + ci];
+        }
+        gp = 2.0 * s;
+    }
+    C.c0 = 0.0;
+    if constexpr (Lay::REG) {
+        // lower triangle of H_FF, packed index e -> (p >= q), built by all lanes into the
+        // (still empty) R buffer, then lane p loads row p; rows/cols >= nf are padded with
+        // the identity so the register factorization runs without predicates
+        double *Hb = C.L.R;
+        if (ok) {
+            const int E = nf * (nf + 1) / 2;
+            for (int e = ln; e < E; e += kWave) {
+                int p = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+                while (p * (p + 1) / 2 > e) --p;
+                while ((p + 1) * (p + 2) / 2 <= e) ++p;
+                const int q = e - p * (p + 1) / 2;
+                Hb[q * LD + p] = H_entry(C.L.fid[p], C.L.fid[q]);
+            }
+        }
+        wave_sync();
+        double h[NF];
+#pragma unroll
+        for (int q = 0; q < NF; ++q) {
+            const bool in = ok && ln < nf && q < nf && q <= ln;
+            h[q] = in ? Hb[q * LD + ln] : ((q == ln) ? 1.0 : 0.0);
+        }
+        wave_sync();
+        MPCQP_STAMP(a.stamps, 3, tst);
+        gi_run_reg<NF>(C, h, gp, D + Lay::oRow);
+    } else {
+        if (ok) {
+            const int E = nf * (nf + 1) / 2;
+            for (int e = ln; e < E; e += kWave) {
+                int p = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+                while (p * (p + 1) / 2 > e) --p;
+                while ((p + 1) * (p + 2) / 2 <= e) ++p;
+                const int q = e - p * (p + 1) / 2;
+                C.L.R[q * LD + p] = H_entry(C.L.fid[p], C.L.fid[q]);
+            }
+            if (ln < nf) C.L.g[ln] = gp;
+        }
+        wave_sync();
+        MPCQP_STAMP(a.stamps, 3, tst);
+        gi_run(C);
+    }
+    MPCQP_STAMP_INIT(tw);
+    SolveOut O;
+    O.x = a.U + (size_t)b * NV;
+    O.cost = a.cost + b;
+    O.status = a.status + b;
+    O.iters = a.iters + b;
+    O.y = nullptr;
+    gi_write(C, O);
+    MPCQP_STAMP(a.stamps, 9, tw);
+    (void)NS;
+}
+
+}  // namespace mpcqp

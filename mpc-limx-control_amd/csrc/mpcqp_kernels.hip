@@ -23,6 +23,7 @@
 #include "../../include/mpcqp.h"
 #include "condense.hpp"
 #include "fused.hpp"
+#include "mpc_fused.hpp"
 #include "gi_solver.hpp"
 
 using namespace mpcqp;
@@ -210,9 +211,16 @@ __global__ void __launch_bounds__(64) k_condense_solve(FastArgs a) {
     fast_condense_solve<NX, NU, N, MODEL, FRIC, NFMAX>(a, smem_c);
 }
 
+template <int NU, int N, int MODEL, bool FRIC, int NF>
+__global__ void __launch_bounds__(64) k_mpc(MpcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_m[];
+    if ((int)blockIdx.x >= a.B) return;
+    fast_mpc<NU, N, MODEL, FRIC, NF>(a, smem_m);
+}
+
 struct FastKernels {
-    const void *disc = nullptr, *cs = nullptr;
-    size_t disc_lds = 0, cs_lds = 0;
+    const void *disc = nullptr, *cs = nullptr, *mpc = nullptr;
+    size_t disc_lds = 0, cs_lds = 0, mpc_lds = 0;
     int nx = 0, nu = 0;
 };
 
@@ -223,6 +231,8 @@ FastKernels make_fast() {
     k.cs = (const void *)&k_condense_solve<NX, NU, N, MODEL, FRIC, NFMAX>;
     k.disc_lds = sizeof(double) * disc_lds_doubles<NX, NU>();
     k.cs_lds = CSLayout<NX, NU, N, FRIC, NFMAX>::lds_bytes;
+    k.mpc = (const void *)&k_mpc<NU, N, MODEL, FRIC, NFMAX>;
+    k.mpc_lds = MpcLayout<NU, N, FRIC, NFMAX>::lds_bytes;
     k.nx = NX;
     k.nu = NU;
     return k;
@@ -323,6 +333,7 @@ struct mpcqp_ctx {
     double *dqd = nullptr, *dpd = nullptr;  // diagonals of Q, P
     double *dAB = nullptr;                  // [B][nx*(nx+nu)] discretised model scratch
     size_t ab_cap = 0;
+    unsigned long long *dstamps = nullptr;  // diagnostic phase cycles (stamps build)
 };
 
 extern "C" {
@@ -589,6 +600,30 @@ int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
 
 int mpcqp_ctx_fast_path(const mpcqp_ctx *c) { return c && c->fast ? 1 : 0; }
 
+int mpcqp_debug_phase_cycles(mpcqp_ctx *c, uint64_t *out, int n) {
+#ifdef MPCQP_STAMPS
+    if (!c || !out || n <= 0) return MPCQP_ERR_BAD_ARG;
+    const int slots = 16;
+    if (!c->dstamps) {
+        if (hipMalloc(&c->dstamps, sizeof(unsigned long long) * slots) != hipSuccess ||
+            hipMemset(c->dstamps, 0, sizeof(unsigned long long) * slots) != hipSuccess)
+            return MPCQP_ERR_DEVICE;
+        for (int i = 0; i < n; ++i) out[i] = 0;
+        return MPCQP_OK;
+    }
+    unsigned long long h[16];
+    if (hipStreamSynchronize(c->stream) != hipSuccess ||
+        hipMemcpy(h, c->dstamps, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemset(c->dstamps, 0, sizeof(h)) != hipSuccess)
+        return MPCQP_ERR_DEVICE;
+    for (int i = 0; i < n; ++i) out[i] = i < slots ? h[i] : 0;
+    return MPCQP_OK;
+#else
+    (void)c; (void)out; (void)n;
+    return MPCQP_ERR_BAD_ARG;  // only the diagnostic build (libmpcqp_stamps.so) records
+#endif
+}
+
 int mpcqp_ctx_destroy(mpcqp_ctx *c) {
     if (!c) return MPCQP_ERR_BAD_ARG;
     hipSetDevice(c->device);
@@ -599,6 +634,7 @@ int mpcqp_ctx_destroy(mpcqp_ctx *c) {
     hipFree(c->dqd);
     hipFree(c->dpd);
     hipFree(c->dAB);
+    hipFree(c->dstamps);
     hipFree(c->scratchH);
     hipFree(c->scratchF);
     if (c->ev_ok)
@@ -679,6 +715,30 @@ static FastArgs fast_args(mpcqp_ctx *c, int B) {
     a.mu = m.mu;
     a.max_iter = m.max_iter;
     a.max_free = m.max_free > 0 ? m.max_free : m.nu * m.N;
+    a.stamps = c->dstamps;
+    return a;
+}
+
+static MpcArgs mpc_args(mpcqp_ctx *c, int B) {
+    MpcArgs a;
+    memset(&a, 0, sizeof(a));
+    const mpcqp_model &m = c->m;
+    a.B = B;
+    a.Ts = m.Ts;
+    a.mass = m.mass;
+    for (int i = 0; i < 9; ++i) a.Ibinv[i] = c->Ibinv[i];
+    a.qd = c->dqd;
+    a.pd = c->dpd;
+    a.rmat = c->dR;
+    a.fz_min = m.fz_min;
+    a.fz_max = m.fz_max;
+    a.fxy_max = m.fxy_max;
+    a.u_min = m.u_min;
+    a.u_max = m.u_max;
+    a.mu = m.mu;
+    a.max_iter = m.max_iter;
+    a.max_free = m.max_free > 0 ? m.max_free : m.nu * m.N;
+    a.stamps = c->dstamps;
     return a;
 }
 
@@ -829,6 +889,23 @@ int mpcqp_batch_solve(mpcqp_ctx *c, int B, const double *x0, const double *xref,
     if (!c) return MPCQP_ERR_BAD_ARG;
     if (B <= 0) return B == 0 ? MPCQP_OK : MPCQP_ERR_BAD_ARG;
     hipSetDevice(c->device);
+    if (c->fast) {  // one fused kernel: closed-form linearise/discretise/condense + solve
+        if (!x0 || !xref || !lin || !U || !cost || !status || !iters) return MPCQP_ERR_BAD_ARG;
+        if (c->m.model == MPCQP_MODEL_SRBM && !contact) return MPCQP_ERR_BAD_ARG;
+        MpcArgs a = mpc_args(c, B);
+        a.lin = lin;
+        a.x0 = x0;
+        a.xref = xref;
+        a.contact = contact;
+        a.U = U;
+        a.cost = cost;
+        a.status = status;
+        a.iters = iters;
+        tbegin(c, 1);
+        const int rc = launch(c->fk.mpc, B, c->fk.mpc_lds, c->stream, &a);
+        tend(c, 1);
+        return rc;
+    }
     const size_t ab = (size_t)c->m.nx * (c->m.nx + c->m.nu);
     if (c->ab_cap < (size_t)B) {
         hipFree(c->dAB);

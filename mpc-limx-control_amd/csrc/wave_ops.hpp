@@ -63,4 +63,32 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Code-motion fence for unrolled straight-line phases: no memory access moves across it at
+// the IR level (empty asm with a memory clobber) nor in the machine scheduler.
+__device__ __forceinline__ void step_fence() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// Materialise v in a VGPR at this point: arithmetic producing v cannot sink past it.
+__device__ __forceinline__ void pin(double &v) { asm volatile("" : "+v"(v)); }
+
+// Diagnostic phase stamps (built only with -DMPCQP_STAMPS, lib/libmpcqp_stamps.so): cycles
+// (s_memtime) since the previous stamp are added to slot k of a global array.  The real
+// library compiles these to nothing.
+#ifdef MPCQP_STAMPS
+#define MPCQP_STAMP(ptr, k, t)                                                  \
+    do {                                                                        \
+        if (ptr) {                                                              \
+            const unsigned long long now_ = __builtin_amdgcn_s_memtime();      \
+            if (::mpcqp::lane() == 0) atomicAdd(&(ptr)[(k)], now_ - (t));      \
+            (t) = now_;                                                         \
+        }                                                                       \
+    } while (0)
+#define MPCQP_STAMP_INIT(t) unsigned long long t = __builtin_amdgcn_s_memtime()
+#else
+#define MPCQP_STAMP(ptr, k, t) ((void)0)
+#define MPCQP_STAMP_INIT(t) ((void)0)
+#endif
+
 }  // namespace mpcqp

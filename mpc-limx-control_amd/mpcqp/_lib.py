@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_PKG), "lib", "libmpcqp.so")
+LIB_PATH = os.environ.get("MPCQP_LIB") or os.path.join(os.path.dirname(_PKG), "lib",
+                                                       "libmpcqp.so")
 
 MPCQP_OK = 0
 STATUS = {0: "OK", 1: "BAD_DIMS", 2: "INFEASIBLE", 3: "ITER_LIMIT", 4: "NOT_PD", 5: "DEVICE",
@@ -24,6 +25,7 @@ EXPORTS = [
     "mpcqp_ctx_create", "mpcqp_ctx_destroy", "mpcqp_set_stream", "mpcqp_sync",
     "mpcqp_batch_condense", "mpcqp_batch_solve_qp", "mpcqp_batch_solve",
     "mpcqp_ctx_fast_path", "mpcqp_batch_discretize", "mpcqp_batch_condense_solve",
+    "mpcqp_debug_phase_cycles",
     "mpcqp_batch_select_min", "mpcqp_enable_timing", "mpcqp_last_kernel_ms",
     "mpcqp_status_string", "mpcqp_device_count",
 ]
@@ -71,6 +73,7 @@ def lib():
     L.mpcqp_batch_solve_qp.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp]
     L.mpcqp_batch_solve.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp]
     L.mpcqp_ctx_fast_path.argtypes = [vp]
+    L.mpcqp_debug_phase_cycles.argtypes = [vp, vp, i]
     L.mpcqp_batch_discretize.argtypes = [vp, i, vp, vp]
     L.mpcqp_batch_condense_solve.argtypes = [vp, i] + [vp] * 8
     L.mpcqp_batch_select_min.argtypes = [vp, i, vp, vp, C.c_int64, vp]
