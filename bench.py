@@ -49,6 +49,18 @@ def algorithmic_bytes(nx: int, nu: int, N: int):
     return (nx + nx * (N + 1) + 7 + 2 * N + nV + 1) * 8 + 4
 
 
+def pmc_traffic(config: str, batch: int):
+    """HBM bytes per k_mpc launch from the committed rocprofv3 PMC summary
+    (tools/profile_run.sh + tools/summarize_profile.py), if it matches this workload."""
+    try:
+        t = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    except (OSError, ValueError):
+        return None, None
+    if t.get("config") != config or t.get("batch") != batch:
+        return None, None
+    return t.get("hbm_bytes_per_launch"), t.get("tag")
+
+
 def cpu_baseline(p, batch, budget_s=12.0):
     """The oracle (C restatement of the reference path, OpenMP over the batch) on the host."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -86,7 +98,8 @@ def main():
     import torch.distributed as dist
 
     import mpcqp
-    from mpcqp.engine import BatchEngine, decode_key
+    from mpcqp.dist import select_global
+    from mpcqp.engine import BatchEngine
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -107,12 +120,7 @@ def main():
         eng.solve(d)
         key = eng.select_min(d, index_base=rank * B)
         if world > 1:
-            dist.all_reduce(key, op=dist.ReduceOp.MIN)
-            _, gidx = decode_key(int(key.item()))
-            owner = gidx // B
-            if owner == rank:
-                ubest.copy_(d["U"][gidx % B])
-            dist.broadcast(ubest, src=owner)
+            select_global(dist, key, d["U"], B, ubest)
 
     for _ in range(args.warmup):
         step()
@@ -132,12 +140,7 @@ def main():
         key = eng.select_min(d, index_base=rank * B)
         e[3].record(stream)
         if world > 1:
-            dist.all_reduce(key, op=dist.ReduceOp.MIN)
-            _, gidx = decode_key(int(key.item()))
-            owner = gidx // B
-            if owner == rank:
-                ubest.copy_(d["U"][gidx % B])
-            dist.broadcast(ubest, src=owner)
+            select_global(dist, key, d["U"], B, ubest)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -160,6 +163,7 @@ def main():
         f_qp = fl["condense"] + fl["solve_fixed"] + fl["per_iter"] * float(iters.mean())
         dom_flops = f_qp * B
         achieved = dom_flops / (mpc_ms * 1e-3) / 1e12
+        traffic, traffic_tag = pmc_traffic(args.config, B)
         out = dict(
             metric="QP solves/sec, 13-state N=10 SRBM MPC, batch=65536 at 1/2/4/8 MI355X",
             value=total / (elapsed / args.steps), unit="QP/s", n_gpus=world, steps=args.steps,
@@ -176,7 +180,11 @@ def main():
                         kernel_ms=dict(k_mpc=mpc_ms, k_select_min=sel_ms)),
             roofline=dict(bound="mfma", kernel="k_mpc", achieved=achieved,
                           peak=FP64_PEAK_TFLOPS, unit="TFLOP/s",
-                          frac=achieved / FP64_PEAK_TFLOPS, traffic=None,
+                          frac=achieved / FP64_PEAK_TFLOPS, traffic=traffic,
+                          traffic_source=(f"profiles/{traffic_tag}_summary.json (rocprofv3 PMC, "
+                                          "2 x FETCH_SIZE + WRITE_SIZE)") if traffic else None,
+                          algorithmic_bytes_per_launch=algorithmic_bytes(
+                              p["nx"], p["nu"], p["N"]) * B,
                           algorithmic_flops_per_qp=f_qp,
                           whole_step_tflops=dom_flops / (ms_per_step * 1e-3) / 1e12),
         )

@@ -153,6 +153,13 @@ int mpcqp_batch_solve_qp(mpcqp_ctx *ctx, int B, const double *H, const double *f
 int mpcqp_batch_solve(mpcqp_ctx *ctx, int B, const double *x0, const double *xref,
                       const double *lin, const uint64_t *contact, double *U, double *cost,
                       int *status, int *iters);
+/* Host-pointer convenience for controllers (one tick, B = 1 state x C candidates): copies the
+ * host arrays (same layouts as above) into context-owned device buffers, runs
+ * mpcqp_batch_solve and copies U/cost/status/iters back; synchronous. */
+int mpcqp_batch_solve_host(mpcqp_ctx *ctx, int B, const double *x0, const double *xref,
+                           const double *lin, const uint64_t *contact, double *U, double *cost,
+                           int *status, int *iters);
+
 /* key = (order-preserving bits of (float)cost << 31) | (index_base + i), min over the batch,
  * written to *key (device int64).  Instances with status != OK never win.  The caller
  * reduces keys across ranks with one MIN all-reduce (RCCL). */

@@ -334,6 +334,9 @@ struct mpcqp_ctx {
     double *dAB = nullptr;                  // [B][nx*(nx+nu)] discretised model scratch
     size_t ab_cap = 0;
     unsigned long long *dstamps = nullptr;  // diagnostic phase cycles (stamps build)
+    // host-pointer entry point staging
+    void *hbuf = nullptr;
+    size_t hbuf_cap = 0;
 };
 
 extern "C" {
@@ -635,6 +638,7 @@ int mpcqp_ctx_destroy(mpcqp_ctx *c) {
     hipFree(c->dpd);
     hipFree(c->dAB);
     hipFree(c->dstamps);
+    hipFree(c->hbuf);
     hipFree(c->scratchH);
     hipFree(c->scratchF);
     if (c->ev_ok)
@@ -917,6 +921,46 @@ int mpcqp_batch_solve(mpcqp_ctx *c, int B, const double *x0, const double *xref,
     int rc = mpcqp_batch_discretize(c, B, lin, c->dAB);
     if (rc) return rc;
     return mpcqp_batch_condense_solve(c, B, c->dAB, x0, xref, contact, U, cost, status, iters);
+}
+
+int mpcqp_batch_solve_host(mpcqp_ctx *c, int B, const double *x0, const double *xref,
+                           const double *lin, const uint64_t *contact, double *U, double *cost,
+                           int *status, int *iters) {
+    if (!c || !x0 || !xref || !lin || !U || !cost || !status || !iters || B < 0)
+        return MPCQP_ERR_BAD_ARG;
+    if (c->m.model == MPCQP_MODEL_SRBM && !contact) return MPCQP_ERR_BAD_ARG;
+    if (B == 0) return MPCQP_OK;
+    hipSetDevice(c->device);
+    const size_t nx = c->m.nx, N = c->m.N, nV = (size_t)c->m.nu * c->m.N;
+    const size_t n_x0 = nx * B, n_xr = nx * (N + 1) * B, n_lin = 8 * (size_t)B, n_u = nV * B;
+    const size_t bytes = sizeof(double) * (n_x0 + n_xr + n_lin + n_u + B) +
+                         sizeof(uint64_t) * B + 2 * sizeof(int) * B + 64;
+    if (c->hbuf_cap < bytes) {
+        hipFree(c->hbuf);
+        c->hbuf = nullptr;
+        c->hbuf_cap = 0;
+        if (hipMalloc(&c->hbuf, bytes) != hipSuccess) return MPCQP_ERR_DEVICE;
+        c->hbuf_cap = bytes;
+    }
+    double *d_x0 = (double *)c->hbuf, *d_xr = d_x0 + n_x0, *d_lin = d_xr + n_xr,
+           *d_U = d_lin + n_lin, *d_cost = d_U + n_u;
+    uint64_t *d_ct = (uint64_t *)(d_cost + B);
+    int *d_st = (int *)(d_ct + B), *d_it = d_st + B;
+    const hipMemcpyKind h2d = hipMemcpyHostToDevice, d2h = hipMemcpyDeviceToHost;
+    if (hipMemcpyAsync(d_x0, x0, sizeof(double) * n_x0, h2d, c->stream) != hipSuccess ||
+        hipMemcpyAsync(d_xr, xref, sizeof(double) * n_xr, h2d, c->stream) != hipSuccess ||
+        hipMemcpyAsync(d_lin, lin, sizeof(double) * n_lin, h2d, c->stream) != hipSuccess ||
+        (contact && hipMemcpyAsync(d_ct, contact, sizeof(uint64_t) * B, h2d, c->stream) != hipSuccess))
+        return MPCQP_ERR_DEVICE;
+    int rc = mpcqp_batch_solve(c, B, d_x0, d_xr, d_lin, contact ? d_ct : nullptr, d_U, d_cost,
+                               d_st, d_it);
+    if (rc) return rc;
+    if (hipMemcpyAsync(U, d_U, sizeof(double) * n_u, d2h, c->stream) != hipSuccess ||
+        hipMemcpyAsync(cost, d_cost, sizeof(double) * B, d2h, c->stream) != hipSuccess ||
+        hipMemcpyAsync(status, d_st, sizeof(int) * B, d2h, c->stream) != hipSuccess ||
+        hipMemcpyAsync(iters, d_it, sizeof(int) * B, d2h, c->stream) != hipSuccess)
+        return MPCQP_ERR_DEVICE;
+    return hip_status(hipStreamSynchronize(c->stream));
 }
 
 int mpcqp_batch_select_min(mpcqp_ctx *c, int B, const double *cost, const int *status,

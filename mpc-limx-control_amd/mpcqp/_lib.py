@@ -25,7 +25,7 @@ EXPORTS = [
     "mpcqp_ctx_create", "mpcqp_ctx_destroy", "mpcqp_set_stream", "mpcqp_sync",
     "mpcqp_batch_condense", "mpcqp_batch_solve_qp", "mpcqp_batch_solve",
     "mpcqp_ctx_fast_path", "mpcqp_batch_discretize", "mpcqp_batch_condense_solve",
-    "mpcqp_debug_phase_cycles",
+    "mpcqp_debug_phase_cycles", "mpcqp_batch_solve_host",
     "mpcqp_batch_select_min", "mpcqp_enable_timing", "mpcqp_last_kernel_ms",
     "mpcqp_status_string", "mpcqp_device_count",
 ]
@@ -74,6 +74,7 @@ def lib():
     L.mpcqp_batch_solve.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp]
     L.mpcqp_ctx_fast_path.argtypes = [vp]
     L.mpcqp_debug_phase_cycles.argtypes = [vp, vp, i]
+    L.mpcqp_batch_solve_host.argtypes = [vp, i] + [vp] * 8
     L.mpcqp_batch_discretize.argtypes = [vp, i, vp, vp]
     L.mpcqp_batch_condense_solve.argtypes = [vp, i] + [vp] * 8
     L.mpcqp_batch_select_min.argtypes = [vp, i, vp, vp, C.c_int64, vp]

@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Summarize a tools/profile_run.sh output directory into profiles/:
+  <tag>_kernel_stats.csv   rocprofv3 --stats summary (copied verbatim)
+  <tag>_summary.json       per-kernel average duration + PMC HBM traffic per launch
+  pmc_traffic.json         the k_mpc traffic figure bench.py reports as roofline.traffic
+HBM bytes follow MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE are KiB,
+collected in separate passes; on gfx950 FETCH_SIZE counts half of the bytes of a coalesced
+stream, so reads are doubled.  Usage: tools/summarize_profile.py PROFDIR TAG [--batch B]"""
+import argparse
+import csv
+import json
+import os
+import shutil
+import statistics as st
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def counter(path, kernel):
+    v = [float(r["Counter_Value"]) for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
+    return st.median(v) if v else None, len(v)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("prof")
+    ap.add_argument("tag")
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--config", default="B")
+    ap.add_argument("--kernel", default="k_mpc")
+    a = ap.parse_args()
+    out = os.path.join(ROOT, "profiles")
+    stats = os.path.join(a.prof, "trace", "run_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(out, f"{a.tag}_kernel_stats.csv"))
+    kern = {r["Name"]: dict(calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]),
+                            pct=float(r["Percentage"])) for r in csv.DictReader(open(stats))}
+    fetch, nf = counter(os.path.join(a.prof, "fetch", "run_counter_collection.csv"), a.kernel)
+    write, nw = counter(os.path.join(a.prof, "write", "run_counter_collection.csv"), a.kernel)
+    traffic = None
+    if fetch is not None and write is not None:
+        traffic = 2.0 * fetch * 1024 + write * 1024
+    summ = dict(tag=a.tag, kernel=a.kernel, config=a.config, batch=a.batch, kernels=kern,
+                fetch_size_kib_median=fetch, write_size_kib_median=write, fetch_samples=nf,
+                write_samples=nw, hbm_bytes_per_launch=traffic,
+                correction="reads = 2 x FETCH_SIZE (gfx950 half-count), writes = WRITE_SIZE")
+    json.dump(summ, open(os.path.join(out, f"{a.tag}_summary.json"), "w"), indent=1)
+    json.dump(dict(config=a.config, batch=a.batch, kernel=a.kernel, tag=a.tag,
+                   hbm_bytes_per_launch=traffic), open(os.path.join(out, "pmc_traffic.json"), "w"),
+              indent=1)
+    print(json.dumps(summ, indent=1)[:1500])
+
+
+if __name__ == "__main__":
+    main()
