@@ -74,13 +74,49 @@ def cpu_baseline(p, batch, budget_s=12.0):
     rate0 = n0 / max(1e-6, time.perf_counter() - t)
     n = int(min(batch["x0"].shape[0], max(n0, rate0 * budget_s)))
     sub = {k: v[:n] for k, v in batch.items()}
+    # repeat the sample until ~budget_s of CPU work is timed (10-30 s guideline)
+    o, done, dt, passes = None, 0, 0.0, 0
+    while passes == 0 or (dt < budget_s and passes < 8):
+        t = time.perf_counter()
+        r = oracle.srbm_batch(p, sub["x0"], sub["xref"], sub["lin"], sub["contact"],
+                              nthreads=threads)
+        dt += time.perf_counter() - t
+        done += n
+        passes += 1
+        o = o if o is not None else r
+    n1 = min(n, max(16, int(done / dt / threads * 2.0)))  # ~2 s single-thread sample
     t = time.perf_counter()
-    o = oracle.srbm_batch(p, sub["x0"], sub["xref"], sub["lin"], sub["contact"], nthreads=threads)
-    dt = time.perf_counter() - t
-    return dict(value=n / dt, unit="QP/s", cores=threads, kind="port",
-                sample=f"first {n} instances of the rank-0 batch, oracle/mpcqp_oracle.c "
-                       f"(reference-literal dense condensing + Goldfarb-Idnani), OpenMP "
-                       f"{threads} threads, {dt:.1f} s"), o
+    oracle.srbm_batch(p, sub["x0"][:n1], sub["xref"][:n1], sub["lin"][:n1], sub["contact"][:n1],
+                      nthreads=1)
+    one = n1 / (time.perf_counter() - t)
+    return dict(value=done / dt, unit="QP/s", cores=threads, kind="port",
+                single_thread_value=one,
+                sample=f"first {n} instances of the rank-0 batch x {passes} passes, "
+                       f"oracle/mpcqp_oracle.c (reference-literal dense condensing + "
+                       f"Goldfarb-Idnani), OpenMP {threads} threads, {dt:.1f} s"), o
+
+
+def host_staged_rate(eng, batch, p, reps=5):
+    """QP/s through mpcqp_batch_solve_host: host arrays in, H2D + k_mpc + D2H, synchronous
+    (the PCIe-inclusive number; never `value`)."""
+    import ctypes as C
+
+    from mpcqp._lib import lib
+    B = batch["x0"].shape[0]
+    nV = p["nu"] * p["N"]
+    U = np.zeros(B * nV)
+    cost = np.zeros(B)
+    st = np.zeros(B, np.int32)
+    it = np.zeros(B, np.int32)
+    ins = [np.ascontiguousarray(batch[k]) for k in ("x0", "xref", "lin", "contact")]
+    ptr = lambda a: C.c_void_p(a.ctypes.data)
+    call = lambda: lib().mpcqp_batch_solve_host(eng.ctx, B, *[ptr(a) for a in ins], ptr(U),
+                                                 ptr(cost), ptr(st), ptr(it))
+    assert call() == 0
+    t = time.perf_counter()
+    for _ in range(reps):
+        call()
+    return B * reps / (time.perf_counter() - t)
 
 
 def main():
@@ -188,6 +224,7 @@ def main():
                           algorithmic_flops_per_qp=f_qp,
                           whole_step_tflops=dom_flops / (ms_per_step * 1e-3) / 1e12),
         )
+        out["config"]["pcie_inclusive_qps"] = host_staged_rate(eng, batch, p)
         if not args.no_cpu_baseline:
             cb, _ = cpu_baseline(p, batch)
             out["cpu_baseline"] = cb

@@ -124,6 +124,7 @@ __device__ __forceinline__ void fast_condense_solve(const FastArgs &a, unsigned 
     MPCQP_STAMP_INIT(tst);
     GiCtx C;
     C.stamps = a.stamps;
+    C.cut = 0;
     C.P = &P;
     C.nfmax = NFMAX;
     C.L.ld = LD;

@@ -107,7 +107,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         }
         if (bad) status = ST_NOT_PD;
     }
-    MPCQP_STAMP(C.stamps, 5, tst);
+    MPCQP_STAMP(C.stamps, 5, tst); MPCQP_CUT(C.cut, 4);
     if (status == ST_OK && nf > 0) {
         // ---- park L in the (still empty) R buffer: lane i stores row i, L(i,l) at l*ld + i
 #pragma unroll
@@ -127,7 +127,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             pin(Jr[i]);
             step_fence();  // keep step i's loads and arithmetic in step i
         }
-        MPCQP_STAMP(C.stamps, 6, tst);
+        MPCQP_STAMP(C.stamps, 6, tst); MPCQP_CUT(C.cut, 5);
         // ---- unconstrained minimum x = -J t, objective -|t|^2/2
         double s = 0.0, tt = 0.0;
 #pragma unroll
@@ -147,7 +147,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         if (ln < nf) L.xs[ln] = x;
         wave_sync();
     }
-    MPCQP_STAMP(C.stamps, 7, tst);
+    MPCQP_STAMP(C.stamps, 7, tst); MPCQP_CUT(C.cut, 6);
 
     const int max_iter = P.max_iter > 0 ? P.max_iter : 10 * (mt + nf + 1);
     bool done = (status != ST_OK) || nf == 0;
@@ -170,8 +170,9 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         for (;;) {
             if (iters >= max_iter) { status = ST_ITER_LIMIT; done = true; break; }
             ++iters;
-            const double dd = wave_sum(ln < nf ? dj * dj : 0.0);
-            const double zn = wave_sum((ln >= q && ln < nf) ? dj * dj : 0.0);
+            double dd = ln < nf ? dj * dj : 0.0;
+            double zn = (ln >= q && ln < nf) ? dj * dj : 0.0;
+            wave_sum2(dd, zn);
             double z = 0.0;
 #pragma unroll
             for (int j = 0; j < NF; ++j)
@@ -203,26 +204,39 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                 if (ln == q) u += t;
                 if (t2 <= t1) {
                     // ---- add p: Givens chain on d from the bottom up to q+1, applied to the
-                    //      J columns held in registers
-                    double acc = readlane(dj, nf - 1);
+                    //      J columns held in registers.  The chain's running norm is the
+                    //      suffix norm of d, so every rotation (c_j, s_j) comes from suffix
+                    //      sums of squares in parallel, lane j owning rotation j:
+                    //        acc_j = d_j if T_{j+1} == 0 else sqrt(T_j),  T_j = sum_{i>=j} d_i^2
+                    //        rotation j mixes (j-1, j): hh = sqrt(T_{j-1}), c = d_{j-1}/hh,
+                    //        s = acc_j/hh (identity when acc_j == 0)
+                    double tm1 = 0.0, t0 = 0.0, tp1 = 0.0, dm1 = 0.0;
+#pragma unroll
+                    for (int i = NF - 1; i >= 0; --i) {
+                        const double di = readlane(dj, i);  // 0 beyond nf
+                        const double d2 = di * di;
+                        if (i >= ln - 1) tm1 += d2;
+                        if (i >= ln) t0 += d2;
+                        if (i >= ln + 1) tp1 += d2;
+                        if (i == ln - 1) dm1 = di;
+                    }
+                    const double accl = (tp1 == 0.0) ? dj : sqrt(t0);
+                    double cl = 1.0, sl = 0.0;
+                    if (accl != 0.0) {
+                        const double ih = 1.0 / sqrt(tm1);
+                        cl = dm1 * ih;
+                        sl = accl * ih;
+                    }
 #pragma unroll
                     for (int j = NF - 1; j >= 1; --j) {
                         if (j > q && j < nf) {
-                            const double a = readlane(dj, j - 1);
-                            double c = 1.0, s = 0.0, hh = a;
-                            if (acc != 0.0) {
-                                hh = sqrt(a * a + acc * acc);
-                                const double ih = 1.0 / hh;
-                                c = a * ih;
-                                s = acc * ih;
-                            }
-                            acc = hh;
+                            const double c = readlane(cl, j), s = readlane(sl, j);
                             const double x0 = Jr[j - 1], x1 = Jr[j];
                             Jr[j - 1] = c * x0 + s * x1;
                             Jr[j] = -s * x0 + c * x1;
                         }
                     }
-                    const double rqq = (q < nf - 1) ? acc : readlane(dj, q);
+                    const double rqq = readlane(accl, q);
                     if (ln < q) L.R[q * ld + ln] = dj;
                     if (ln == q) { L.R[q * ld + q] = rqq; act = p; }
                     if (ln == 0) L.st[p] = 2;
@@ -272,7 +286,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             gi_project_reg<NF>(C, Jr, p, x, dj, sp, rowbuf);
         }
     }
-    MPCQP_STAMP(C.stamps, 8, tst);
+    MPCQP_STAMP(C.stamps, 8, tst); MPCQP_CUT(C.cut, 7);
     C.status = status;
     C.x = x;
     C.u = u;

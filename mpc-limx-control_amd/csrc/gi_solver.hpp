@@ -109,6 +109,7 @@ struct GiCtx {
     double x, u, fval;
     int act, q, iters;
     unsigned long long *stamps;  // diagnostic phase cycles (nullptr: off)
+    int cut;                     // diagnostic cuts build only
 };
 
 __device__ __forceinline__ double rowA(const SolveProblem &P, int r, int v) {
@@ -365,7 +366,7 @@ __device__ __forceinline__ void gi_run(GiCtx &C) {
             }
         C.c0 = wave_sum(cl);
     }
-    MPCQP_STAMP(C.stamps, 5, tst);
+    MPCQP_STAMP(C.stamps, 5, tst); MPCQP_CUT(C.cut, 4);
 
     if (status == ST_OK && nf > 0) {
         // J = L^-T: lane c computes column c of L^-1 and stores Linv(i, c) at J[i*ld + c],
@@ -379,7 +380,7 @@ __device__ __forceinline__ void gi_run(GiCtx &C) {
             }
         }
         wave_sync();
-        MPCQP_STAMP(C.stamps, 6, tst);
+        MPCQP_STAMP(C.stamps, 6, tst); MPCQP_CUT(C.cut, 5);
         // unconstrained minimum x = -J J' g
         double w = 0.0;
         if (ln < nf)
@@ -394,7 +395,7 @@ __device__ __forceinline__ void gi_run(GiCtx &C) {
         if (ln < nf) L.xs[ln] = x;
         wave_sync();
     }
-    MPCQP_STAMP(C.stamps, 7, tst);
+    MPCQP_STAMP(C.stamps, 7, tst); MPCQP_CUT(C.cut, 6);
 
     const int max_iter = P.max_iter > 0 ? P.max_iter : 10 * (mt + nf + 1);
     int eq_next = 2 * nf + nfric;  // dense rows are the only equality candidates
@@ -428,8 +429,9 @@ __device__ __forceinline__ void gi_run(GiCtx &C) {
         for (;;) {
             if (iters >= max_iter) { status = ST_ITER_LIMIT; done = true; break; }
             ++iters;
-            const double dd = wave_sum(ln < nf ? dj * dj : 0.0);
-            const double zn = wave_sum((ln >= q && ln < nf) ? dj * dj : 0.0);
+            double dd = ln < nf ? dj * dj : 0.0;
+            double zn = (ln >= q && ln < nf) ? dj * dj : 0.0;
+            wave_sum2(dd, zn);
             // z = J(:, q:) d(q:)   (lane i)
             double z = 0.0;
             for (int j = q; j < nf; ++j) {
@@ -540,7 +542,7 @@ __device__ __forceinline__ void gi_run(GiCtx &C) {
             gi_cons_project(C, p, x, dj, sp);
         }
     }
-    MPCQP_STAMP(C.stamps, 8, tst);
+    MPCQP_STAMP(C.stamps, 8, tst); MPCQP_CUT(C.cut, 7);
     C.status = status;
     C.x = x;
     C.u = u;
@@ -599,6 +601,7 @@ __device__ __forceinline__ void wave_gi_solve(const SolveProblem &P, const Solve
                                      unsigned char *smem, int nfmax) {
     GiCtx C;
     C.stamps = nullptr;
+    C.cut = 0;
     C.P = &P;
     C.L = gi_carve(smem, nfmax, P.nV, P.mA);
     C.nfmax = nfmax;

@@ -40,6 +40,7 @@ struct MpcArgs {
     double *U, *cost;
     int *status, *iters;
     unsigned long long *stamps;
+    int cut;  // diagnostic cuts build only
 };
 
 template <int NU, int N, bool FRIC, int NF>
@@ -109,6 +110,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     P.max_iter = a.max_iter;
     GiCtx C;
     C.stamps = a.stamps;
+    C.cut = a.cut;
     C.P = &P;
     C.nfmax = NF;
     C.L.ld = LD;
@@ -194,6 +196,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     if (C.nf > a.max_free) C.status = ST_BAD_DIMS;
     wave_sync();
     MPCQP_STAMP(a.stamps, 0, tst);
+    MPCQP_CUT(a.cut, 1);
 
     // ---- S^W_rs = X_r' W X_s   (w: 0 = Q, 1 = P), stored [w][r][s][cj][ci]; the block
     //      loop is wave-uniform so the weights are scalar loads
@@ -227,6 +230,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     }
     wave_sync();
     MPCQP_STAMP(a.stamps, 1, tst);
+    MPCQP_CUT(a.cut, 2);
 
     // ---- H_FF (lane p builds row p) and g
     const int nf = C.nf;
@@ -278,6 +282,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
         }
         wave_sync();
         MPCQP_STAMP(a.stamps, 3, tst);
+        MPCQP_CUT(a.cut, 3);
         gi_run_reg<NF>(C, h, gp, D + Lay::oRow);
     } else {
         if (ok) {
@@ -293,8 +298,12 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
         }
         wave_sync();
         MPCQP_STAMP(a.stamps, 3, tst);
+        MPCQP_CUT(a.cut, 3);
         gi_run(C);
     }
+#ifdef MPCQP_CUTS
+    if (a.cut >= 4 && a.cut <= 7) return;
+#endif
     MPCQP_STAMP_INIT(tw);
     SolveOut O;
     O.x = a.U + (size_t)b * NV;

@@ -743,6 +743,10 @@ static MpcArgs mpc_args(mpcqp_ctx *c, int B) {
     a.max_iter = m.max_iter;
     a.max_free = m.max_free > 0 ? m.max_free : m.nu * m.N;
     a.stamps = c->dstamps;
+    a.cut = 0;
+#ifdef MPCQP_CUTS
+    if (const char *e = getenv("MPCQP_CUT")) a.cut = atoi(e);
+#endif
     return a;
 }
 

@@ -24,34 +24,87 @@ __device__ __forceinline__ int readlane(int v, int src) {
     return __builtin_amdgcn_readlane(v, src);
 }
 
+// ---- reductions: DPP within each 16-lane row (xor 1, xor 2, half-row mirror, row mirror:
+//      after the four steps every lane of a row holds the row's result, bit-identical because
+//      each step combines a pair symmetrically), then the four row results are read into
+//      SGPRs and combined in a fixed order, so the result is wave-uniform.  No LDS traffic
+//      (ds_bpermute costs an LDS round trip per step).
+constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141; // lane i <- lane 7-i within each 8
+constexpr int kDppMirror = 0x140;     // lane i <- lane 15-i within each 16
+
+template <int CTRL>
+__device__ __forceinline__ int dpp(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = dpp<CTRL>((int)(b & 0xffffffffll));
+    const int hi = dpp<CTRL>((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-    return v;
+    v += dpp<kDppXor1>(v);
+    v += dpp<kDppXor2>(v);
+    v += dpp<kDppHalfMirror>(v);
+    v += dpp<kDppMirror>(v);
+    return (readlane(v, 0) + readlane(v, 16)) + (readlane(v, 32) + readlane(v, 48));
+}
+// two independent sums in one pass (the DPP chains interleave)
+__device__ __forceinline__ void wave_sum2(double &a, double &b) {
+    a += dpp<kDppXor1>(a);
+    b += dpp<kDppXor1>(b);
+    a += dpp<kDppXor2>(a);
+    b += dpp<kDppXor2>(b);
+    a += dpp<kDppHalfMirror>(a);
+    b += dpp<kDppHalfMirror>(b);
+    a += dpp<kDppMirror>(a);
+    b += dpp<kDppMirror>(b);
+    a = (readlane(a, 0) + readlane(a, 16)) + (readlane(a, 32) + readlane(a, 48));
+    b = (readlane(b, 0) + readlane(b, 16)) + (readlane(b, 32) + readlane(b, 48));
 }
 __device__ __forceinline__ double wave_max(double v) {
+    v = fmax(v, dpp<kDppXor1>(v));
+    v = fmax(v, dpp<kDppXor2>(v));
+    v = fmax(v, dpp<kDppHalfMirror>(v));
+    v = fmax(v, dpp<kDppMirror>(v));
+    return fmax(fmax(readlane(v, 0), readlane(v, 16)), fmax(readlane(v, 32), readlane(v, 48)));
+}
+
+template <int CTRL, bool MIN>
+__device__ __forceinline__ void arg_step(double &v, int &idx) {
+    const double ov = dpp<CTRL>(v);
+    const int oi = dpp<CTRL>(idx);
+    const bool take = MIN ? (ov < v || (ov == v && oi < idx)) : (ov > v || (ov == v && oi < idx));
+    v = take ? ov : v;
+    idx = take ? oi : idx;
+}
+template <bool MIN>
+__device__ __forceinline__ void wave_arg(double &v, int &idx) {
+    arg_step<kDppXor1, MIN>(v, idx);
+    arg_step<kDppXor2, MIN>(v, idx);
+    arg_step<kDppHalfMirror, MIN>(v, idx);
+    arg_step<kDppMirror, MIN>(v, idx);
+    double bv = readlane(v, 0);
+    int bi = readlane(idx, 0);
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, kWave));
-    return v;
+    for (int r = 16; r < kWave; r += 16) {
+        const double ov = readlane(v, r);
+        const int oi = readlane(idx, r);
+        const bool take = MIN ? (ov < bv || (ov == bv && oi < bi)) : (ov > bv || (ov == bv && oi < bi));
+        bv = take ? ov : bv;
+        bi = take ? oi : bi;
+    }
+    v = bv;
+    idx = bi;
 }
 // lexicographic (value, index) minimum; lanes with nothing to offer pass (+inf, INT_MAX)
-__device__ __forceinline__ void wave_argmin(double &v, int &idx) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const double ov = __shfl_xor(v, o, kWave);
-        const int oi = __shfl_xor(idx, o, kWave);
-        if (ov < v || (ov == v && oi < idx)) { v = ov; idx = oi; }
-    }
-}
+__device__ __forceinline__ void wave_argmin(double &v, int &idx) { wave_arg<true>(v, idx); }
 // (value, index) maximum with the lowest index winning ties (Eigen maxCoeff semantics)
-__device__ __forceinline__ void wave_argmax(double &v, int &idx) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const double ov = __shfl_xor(v, o, kWave);
-        const int oi = __shfl_xor(idx, o, kWave);
-        if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
-    }
-}
+__device__ __forceinline__ void wave_argmax(double &v, int &idx) { wave_arg<false>(v, idx); }
 
 // Ordering point between phases of a single-wave workgroup.  One wave issues its LDS
 // instructions in program order and the LDS executes them in order, so a store by one lane
@@ -89,6 +142,18 @@ __device__ __forceinline__ void pin(double &v) { asm volatile("" : "+v"(v)); }
 #else
 #define MPCQP_STAMP(ptr, k, t) ((void)0)
 #define MPCQP_STAMP_INIT(t) ((void)0)
+#endif
+
+// Diagnostic phase cuts (built only with -DMPCQP_CUTS, lib/libmpcqp_cuts.so): the kernel
+// returns after phase k when the launch's cut value is k, so timing successive cuts gives
+// each phase's cost at full occupancy (tools/phase_cuts.py).
+#ifdef MPCQP_CUTS
+#define MPCQP_CUT(cutv, k) \
+    do {                   \
+        if ((cutv) == (k)) return; \
+    } while (0)
+#else
+#define MPCQP_CUT(cutv, k) ((void)0)
 #endif
 
 }  // namespace mpcqp
