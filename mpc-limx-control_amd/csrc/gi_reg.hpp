@@ -1,13 +1,15 @@
-// gi_reg.hpp -- register-resident Goldfarb-Idnani solve for up to NF <= 32 free variables.
+// gi_reg.hpp -- register-resident Goldfarb-Idnani solve for up to NF <= 64 free variables.
 //
 // Same algorithm, constraint order and tolerances as gi_run (gi_solver.hpp) and the CPU
 // oracle; only the storage differs:
-//   * lane i holds row i of H_FF, then of L (Cholesky, right-looking, in place) -- h[NF]
-//   * lane c computes column c of L^-1 by forward substitution; since J = L^-T, that column
-//     is row c of J, which lane c keeps in registers -- Jr[NF]
-//   * lane 63 runs the same recurrence on g, yielding t = L^-1 g for free; then the
-//     unconstrained minimum is x = -J t and its objective -|t|^2 / 2
-//   * R stays in LDS (column-major, odd ld), as do x (xs) and the constraint states
+//   * lane i holds row i of H_FF, then of L (Cholesky, right-looking, in place) -- h[NF];
+//     g rides along as an extra column, so the same sweep leaves t = L^-1 g on the lanes
+//   * L is parked in LDS (row-major packed), then lane c computes column c of L^-1 by
+//     forward substitution; since J = L^-T, that column is row c of J, which lane c keeps in
+//     registers -- Jr[NF]; the unconstrained minimum is x = -J t, objective -|t|^2 / 2
+//   * R lives in LDS, column-major packed with one sub-diagonal slot per column (the drop
+//     step's Hessenberg entry), reusing the parked-L space: NF(NF+3)/2 doubles in total
+//   * x is mirrored in LDS (xs) for the constraint sweeps, with the constraint states
 // All loops over columns are unrolled to NF with wave-uniform predicates, so every register
 // index is a compile-time constant (no scratch), and cross-lane reads are v_readlane with
 // constant lane indices.
@@ -15,6 +17,15 @@
 #include "gi_solver.hpp"
 
 namespace mpcqp {
+
+// packed R: column j holds rows 0..j+1 (j+1 = the Hessenberg slot of the drop step)
+__device__ __forceinline__ int roff(int j) { return j * (j + 3) / 2; }
+// packed L (parked for the inverse): row i holds columns 0..i
+__host__ __device__ constexpr int lrow(int i) { return i * (i + 1) / 2; }
+template <int NF>
+struct RegPack {
+    static constexpr int doubles = NF * (NF + 3) / 2;  // >= lrow(NF): L fits in R's space
+};
 
 // Row-broadcast of J: d_j = sum over the (<= 2) nonzero entries of n_p of n_a * J(a, j).
 template <int NF>
@@ -76,74 +87,85 @@ __device__ __forceinline__ void gi_project_reg(const GiCtx &C, const double (&Jr
 // rowbuf: NF doubles of LDS.  Fills C.{status,x,u,fval,act,q,iters}.
 template <int NF>
 __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, double *rowbuf) {
-    static_assert(NF <= 32, "register path holds at most 32 free variables");
+    static_assert(NF <= kWave, "register path holds at most 64 free variables");
     GiLds &L = C.L;
     const SolveProblem &P = *C.P;
-    const int nf = C.nf, ld = L.ld, ln = lane(), mt = C.mt;
+    const int nf = C.nf, ln = lane(), mt = C.mt;
     int status = C.status;
     double fval = 0.0, x = 0.0, u = 0.0;
     int iters = 0, q = 0, act = -1;
     double Jr[NF];
+    double gv = g;     // lane i: g_i, then t_i = (L^-1 g)_i
+    double dinv = 1.0; // lane i: 1 / L(i,i)
     MPCQP_STAMP_INIT(tst);
 
     if (status == ST_OK && nf > 0) {
         // ---- Cholesky, right-looking; lane i owns row i.  h is padded with the identity
-        //      beyond nf, so every step runs unpredicated (upper-triangle junk is never read)
+        //      beyond nf (and g with 0), so every step runs unpredicated (upper-triangle junk
+        //      is never read).  The forward solve L t = g runs in the same sweep.
         bool bad = false;
 #pragma unroll
         for (int k = 0; k < NF; ++k) {
             const double piv = readlane(h[k], k);
             bad |= !(piv > 0.0);
-            const double lkk = sqrt(piv);
-            const double lik = (ln == k) ? lkk : h[k] / lkk;
+            const double ik = rsqrt_nr(piv);
+            const double lkk = piv * ik;
+            const double lik = (ln == k) ? lkk : h[k] * ik;
+            const double tk = readlane(gv, k) * ik;
             h[k] = lik;
+            gv = (ln == k) ? tk : ((ln > k) ? gv - lik * tk : gv);
+            dinv = (ln == k) ? ik : dinv;
 #pragma unroll
             for (int j = 0; j < NF; ++j)
+            {
                 if (j > k) h[j] -= lik * readlane(lik, j);
+                if ((j & 15) == 15) step_fence();  // bound the SGPR broadcasts in flight
+            }
 #pragma unroll
             for (int j = 0; j < NF; ++j)
                 if (j >= k) pin(h[j]);  // step k's updates happen in step k
+            pin(gv);
+            pin(dinv);
             step_fence();
         }
         if (bad) status = ST_NOT_PD;
     }
     MPCQP_STAMP(C.stamps, 5, tst); MPCQP_CUT(C.cut, 4);
     if (status == ST_OK && nf > 0) {
-        // ---- park L in the (still empty) R buffer: lane i stores row i, L(i,l) at l*ld + i
+        // ---- park L in the (still empty) R space, row i at lrow(i); 1/L(i,i) in rowbuf
+        double *Lp = L.R;
+        if (ln < NF) {
 #pragma unroll
-        for (int l = 0; l < NF; ++l)
-            if (ln < NF && l <= ln) L.R[l * ld + ln] = h[l];
+            for (int l = 0; l < NF; ++l)
+                if (l <= ln) Lp[lrow(ln) + l] = h[l];
+            rowbuf[ln] = dinv;
+        }
         wave_sync();
-        // ---- columns of L^-1 (lane c), plus t = L^-1 g on lane 63; L(i,l) are uniform-
-        //      address LDS broadcasts, so only J occupies registers here
+        // ---- columns of L^-1 (lane c); L(i,l) are uniform-address LDS broadcasts, so only
+        //      J occupies registers here.  Lanes >= NF start from 0 and stay 0.
 #pragma unroll
         for (int i = 0; i < NF; ++i) {
-            double s = (ln == 63) ? readlane(g, i) : ((ln == i) ? 1.0 : 0.0);
+            // four partial sums: the dot product is an FMA-latency chain otherwise
+            double s4[4] = {(ln == i) ? 1.0 : 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int l = 0; l < NF; ++l) {
-                if (l < i) s -= L.R[l * ld + i] * Jr[l];
+                if (l < i) s4[l & 3] -= Lp[lrow(i) + l] * Jr[l];
+                if ((l & 15) == 15 && l < i) step_fence();  // bound the loads in flight
             }
-            Jr[i] = s / L.R[i * ld + i];
+            Jr[i] = ((s4[0] + s4[1]) + (s4[2] + s4[3])) * rowbuf[i];
             pin(Jr[i]);
             step_fence();  // keep step i's loads and arithmetic in step i
         }
         MPCQP_STAMP(C.stamps, 6, tst); MPCQP_CUT(C.cut, 5);
-        // ---- unconstrained minimum x = -J t, objective -|t|^2/2
-        double s = 0.0, tt = 0.0;
+        // ---- unconstrained minimum x = -J t, objective -|t|^2/2 (t_j = 0 beyond nf)
+        double s4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int j = 0; j < NF; ++j) {
-            const double tj = readlane(Jr[j], 63);  // t_j = 0 beyond nf (g padded with 0)
-            s += Jr[j] * tj;
-            tt += tj * tj;
+            s4[j & 3] += Jr[j] * readlane(gv, j);
+            if ((j & 15) == 15) step_fence();
         }
-        x = (ln < nf) ? -s : 0.0;
-        fval = -0.5 * tt;
-        // lanes nf..NF-1 keep their identity rows of J (decoupled from the free block);
-        // lanes >= NF (incl. lane 63) hold zeros
-        if (ln >= NF) {
-#pragma unroll
-            for (int j = 0; j < NF; ++j) Jr[j] = 0.0;
-        }
+        x = (ln < nf) ? -((s4[0] + s4[1]) + (s4[2] + s4[3])) : 0.0;
+        fval = -0.5 * wave_sum(ln < nf ? gv * gv : 0.0);
         if (ln < nf) L.xs[ln] = x;
         wave_sync();
     }
@@ -173,16 +195,20 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             double dd = ln < nf ? dj * dj : 0.0;
             double zn = (ln >= q && ln < nf) ? dj * dj : 0.0;
             wave_sum2(dd, zn);
-            double z = 0.0;
+            double z4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int j = 0; j < NF; ++j)
-                if (j >= q) z += Jr[j] * readlane(dj, j);  // d_j = 0 for j >= nf
+            {
+                if (j >= q) z4[j & 3] += Jr[j] * readlane(dj, j);  // d_j = 0 for j >= nf
+                if ((j & 15) == 15) step_fence();
+            }
+            const double z = (z4[0] + z4[1]) + (z4[2] + z4[3]);
             // r = R^-1 d(0:q) (R in LDS)
             double r = 0.0, val = dj;
             for (int j = q - 1; j >= 0; --j) {
-                const double rj = readlane(val, j) / L.R[j * ld + j];
+                const double rj = readlane(val, j) / L.R[roff(j) + j];
                 if (ln == j) r = rj;
-                if (ln < j) val -= L.R[j * ld + ln] * rj;
+                if (ln < j) val -= L.R[roff(j) + ln] * rj;
             }
             const double rmax = wave_max(ln < q ? fabs(r) : 0.0);
             double t1 = INFINITY;
@@ -219,6 +245,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                         if (i >= ln) t0 += d2;
                         if (i >= ln + 1) tp1 += d2;
                         if (i == ln - 1) dm1 = di;
+                        if ((i & 15) == 0) step_fence();
                     }
                     const double accl = (tp1 == 0.0) ? dj : sqrt(t0);
                     double cl = 1.0, sl = 0.0;
@@ -235,10 +262,11 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                             Jr[j - 1] = c * x0 + s * x1;
                             Jr[j] = -s * x0 + c * x1;
                         }
+                        if ((j & 15) == 0) step_fence();
                     }
                     const double rqq = readlane(accl, q);
-                    if (ln < q) L.R[q * ld + ln] = dj;
-                    if (ln == q) { L.R[q * ld + q] = rqq; act = p; }
+                    if (ln < q) L.R[roff(q) + ln] = dj;
+                    if (ln == q) { L.R[roff(q) + q] = rqq; act = p; }
                     if (ln == 0) L.st[p] = 2;
                     ++q;
                     wave_sync();
@@ -256,26 +284,26 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                 if (ln >= k && ln < q) { u = un; act = an; }
             }
             for (int j = k; j < q - 1; ++j) {
-                const double v = (ln <= j + 1) ? L.R[(j + 1) * ld + ln] : 0.0;
+                const double v = (ln <= j + 1) ? L.R[roff(j + 1) + ln] : 0.0;
                 wave_sync();
-                if (ln <= j + 1) L.R[j * ld + ln] = v;
+                if (ln <= j + 1) L.R[roff(j) + ln] = v;
                 wave_sync();
             }
             --q;
 #pragma unroll
             for (int j = 0; j < NF - 1; ++j) {
                 if (j >= k && j < q) {
-                    const double a = L.R[j * ld + j], bb = L.R[j * ld + j + 1];
+                    const double a = L.R[roff(j) + j], bb = L.R[roff(j) + j + 1];
                     if (bb != 0.0) {
                         const double hh = sqrt(a * a + bb * bb);
                         const double ih = 1.0 / hh;
                         const double c = a * ih, s = bb * ih;
                         const int l = j + 1 + ln;
                         double r0 = 0.0, r1 = 0.0;
-                        if (l < q) { r0 = L.R[l * ld + j]; r1 = L.R[l * ld + j + 1]; }
+                        if (l < q) { r0 = L.R[roff(l) + j]; r1 = L.R[roff(l) + j + 1]; }
                         wave_sync();
-                        if (l < q) { L.R[l * ld + j] = c * r0 + s * r1; L.R[l * ld + j + 1] = -s * r0 + c * r1; }
-                        if (ln == 0) { L.R[j * ld + j] = hh; L.R[j * ld + j + 1] = 0.0; }
+                        if (l < q) { L.R[roff(l) + j] = c * r0 + s * r1; L.R[roff(l) + j + 1] = -s * r0 + c * r1; }
+                        if (ln == 0) { L.R[roff(j) + j] = hh; L.R[roff(j) + j + 1] = 0.0; }
                         wave_sync();
                         const double x0 = Jr[j], x1 = Jr[j + 1];
                         Jr[j] = c * x0 + s * x1;

@@ -48,15 +48,16 @@ struct MpcLayout {
     static constexpr int NX = 13, NV = NU * N, LD = NF | 1;
     static constexpr int NFRIC = FRIC ? 4 * N * 2 : 0;
     static constexpr int MT = 2 * NF + NFRIC;
-    static constexpr bool REG = NF <= 32;
+    static constexpr bool REG = NF <= 64;
+    static constexpr int NR = REG ? RegPack<NF>::doubles : NF * LD;
     // doubles
     static constexpr int oX0 = 0;                        // B  (NX x NU)
     static constexpr int oX1 = oX0 + NX * NU;            // AB (NX x NU)
     static constexpr int oS = oX1 + NX * NU;             // S[w][r][s] (8 x NU x NU)
     static constexpr int oUV = oS + 8 * NU * NU;         // u_m, v_m: [(N+1)][2][NU]
     static constexpr int oAx = oUV + (N + 1) * 2 * NU;   // A x0 (NX), A^2 x0 (NX)
-    static constexpr int oR = oAx + 2 * NX;              // R factor (NF x LD)
-    static constexpr int oJ = oR + NF * LD;              // J (LDS solver only)
+    static constexpr int oR = oAx + 2 * NX;              // R factor (packed / NF x LD)
+    static constexpr int oJ = oR + NR;                   // J (LDS solver only)
     static constexpr int oRow = oJ + (REG ? 0 : NF * LD);// row broadcast buffer (NF)
     static constexpr int oG = oRow + NF;                 // g (LDS solver)
     static constexpr int oXS = oG + NF;
@@ -270,7 +271,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
                 while (p * (p + 1) / 2 > e) --p;
                 while ((p + 1) * (p + 2) / 2 <= e) ++p;
                 const int q = e - p * (p + 1) / 2;
-                Hb[q * LD + p] = H_entry(C.L.fid[p], C.L.fid[q]);
+                Hb[e] = H_entry(C.L.fid[p], C.L.fid[q]);  // row-major packed: e = lrow(p) + q
             }
         }
         wave_sync();
@@ -278,7 +279,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
 #pragma unroll
         for (int q = 0; q < NF; ++q) {
             const bool in = ok && ln < nf && q < nf && q <= ln;
-            h[q] = in ? Hb[q * LD + ln] : ((q == ln) ? 1.0 : 0.0);
+            h[q] = in ? Hb[lrow(ln) + q] : ((q == ln) ? 1.0 : 0.0);
         }
         wave_sync();
         MPCQP_STAMP(a.stamps, 3, tst);

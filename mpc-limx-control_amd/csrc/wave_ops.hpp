@@ -123,6 +123,16 @@ __device__ __forceinline__ void step_fence() {
     __builtin_amdgcn_sched_barrier(0);
 }
 
+// 1/sqrt(a) for a > 0: v_rsq_f64 plus two Newton steps (~1 ulp; a short dependency chain
+// compared with the correctly rounded sqrt and divide sequences)
+__device__ __forceinline__ double rsqrt_nr(double a) {
+    double y = __builtin_amdgcn_rsq(a);
+    const double h = 0.5 * a;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
+
 // Materialise v in a VGPR at this point: arithmetic producing v cannot sink past it.
 __device__ __forceinline__ void pin(double &v) { asm volatile("" : "+v"(v)); }
 
@@ -152,6 +162,8 @@ __device__ __forceinline__ void pin(double &v) { asm volatile("" : "+v"(v)); }
     do {                   \
         if ((cutv) == (k)) return; \
     } while (0)
+#elif defined(MPCQP_MARKS)
+#define MPCQP_CUT(cutv, k) asm volatile(";@@CUT " #k)
 #else
 #define MPCQP_CUT(cutv, k) ((void)0)
 #endif
