@@ -27,23 +27,26 @@ struct RegPack {
     static constexpr int doubles = NF * (NF + 3) / 2;  // >= lrow(NF): L fits in R's space
 };
 
-// Row-broadcast of J: d_j = sum over the (<= 2) nonzero entries of n_p of n_a * J(a, j).
+// Row-broadcast of J: d_j = c0 J(a0, j) [+ c1 J(a1, j)] on lane j.  The owning lanes publish
+// their J rows to LDS (buf[0, NF) and buf[NF, 2NF)); every lane reads its column.
 template <int NF>
 __device__ __forceinline__ double reg_project(const double (&Jr)[NF], int a0, double c0,
-                                              int a1, double c1, double *rowbuf) {
+                                              int a1, double c1, double *buf) {
     const int ln = lane();
-    // lane a0 (and a1) publish their rows scaled by the normal's coefficients
     if (ln == a0) {
 #pragma unroll
-        for (int c = 0; c < NF; ++c) rowbuf[c] = c0 * Jr[c];
+        for (int c = 0; c < NF; ++c) buf[c] = Jr[c];
     }
-    wave_sync();
     if (a1 >= 0 && ln == a1) {
 #pragma unroll
-        for (int c = 0; c < NF; ++c) rowbuf[c] += c1 * Jr[c];
+        for (int c = 0; c < NF; ++c) buf[NF + c] = Jr[c];
     }
     wave_sync();
-    const double d = (ln < NF) ? rowbuf[ln] : 0.0;
+    double d = 0.0;
+    if (ln < NF) {
+        d = c0 * buf[ln];
+        if (a1 >= 0) d += c1 * buf[NF + ln];
+    }
     wave_sync();
     return d;
 }
@@ -84,7 +87,9 @@ __device__ __forceinline__ void gi_project_reg(const GiCtx &C, const double (&Jr
 }
 
 // h: lane p holds row p of H_FF (columns < nf meaningful), g: lane p holds g_p.
-// rowbuf: NF doubles of LDS.  Fills C.{status,x,u,fval,act,q,iters}.
+// rowbuf: 4 NF doubles of LDS (16-byte aligned): row / column broadcast buffers and the
+// rotation pairs.  Broadcasts go through LDS (one ds_read_b128 brings two values to every
+// lane) rather than v_readlane pairs, which cost VALU issue slots.  Fills C.{status,x,u,fval,act,q,iters}.
 template <int NF>
 __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, double *rowbuf) {
     static_assert(NF <= kWave, "register path holds at most 64 free variables");
@@ -97,6 +102,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
     double Jr[NF];
     double gv = g;     // lane i: g_i, then t_i = (L^-1 g)_i
     double dinv = 1.0; // lane i: 1 / L(i,i)
+    double *colb = rowbuf + NF, *rot = rowbuf + 2 * NF;
     MPCQP_STAMP_INIT(tst);
 
     if (status == ST_OK && nf > 0) {
@@ -115,11 +121,13 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             h[k] = lik;
             gv = (ln == k) ? tk : ((ln > k) ? gv - lik * tk : gv);
             dinv = (ln == k) ? ik : dinv;
+            if (ln > k && ln < NF) colb[ln] = lik;  // column k of L, broadcast through LDS
+            wave_sync();
 #pragma unroll
             for (int j = 0; j < NF; ++j)
             {
-                if (j > k) h[j] -= lik * readlane(lik, j);
-                if ((j & 15) == 15) step_fence();  // bound the SGPR broadcasts in flight
+                if (j > k) h[j] -= lik * colb[j];
+                if ((j & 7) == 7 && j > k) step_fence();  // bound the loads in flight
             }
 #pragma unroll
             for (int j = 0; j < NF; ++j)
@@ -158,11 +166,13 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         }
         MPCQP_STAMP(C.stamps, 6, tst); MPCQP_CUT(C.cut, 5);
         // ---- unconstrained minimum x = -J t, objective -|t|^2/2 (t_j = 0 beyond nf)
+        if (ln < NF) colb[ln] = gv;
+        wave_sync();
         double s4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int j = 0; j < NF; ++j) {
-            s4[j & 3] += Jr[j] * readlane(gv, j);
-            if ((j & 15) == 15) step_fence();
+            s4[j & 3] += Jr[j] * colb[j];
+            if ((j & 7) == 7) step_fence();
         }
         x = (ln < nf) ? -((s4[0] + s4[1]) + (s4[2] + s4[3])) : 0.0;
         fval = -0.5 * wave_sum(ln < nf ? gv * gv : 0.0);
@@ -171,109 +181,101 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
     }
     MPCQP_STAMP(C.stamps, 7, tst); MPCQP_CUT(C.cut, 6);
 
+    // ---- dual active-set loop, flattened: one pass = one step (add or drop).  J changes in
+    //      exactly one place per pass (a rotation sequence read from LDS), so the register
+    //      allocator sees a single loop-carried definition of Jr.
     const int max_iter = P.max_iter > 0 ? P.max_iter : 10 * (mt + nf + 1);
     bool done = (status != ST_OK) || nf == 0;
+    bool fresh = true;  // select a new violated constraint
+    int p = 0;
     while (!done) {
-        // ---- step 1: most violated inactive constraint (lowest id on ties)
-        double best = INFINITY;
-        int bid = 0x7fffffff;
-        for (int id = ln; id < mt; id += kWave) {
-            if (L.st[id] != 1) continue;
-            const double s = gi_cons_slack_lane(C, id);
-            if (s < -kFeasTol * (1.0 + fabs(gi_cons_b(C, id))) && s < best) { best = s; bid = id; }
+        if (fresh) {
+            // ---- step 1: most violated inactive constraint (lowest id on ties)
+            double best = INFINITY;
+            int bid = 0x7fffffff;
+            for (int id = ln; id < mt; id += kWave) {
+                if (L.st[id] != 1) continue;
+                const double sl_ = gi_cons_slack_lane(C, id);
+                if (sl_ < -kFeasTol * (1.0 + fabs(gi_cons_b(C, id))) && sl_ < best) { best = sl_; bid = id; }
+            }
+            wave_argmin(best, bid);
+            if (bid == 0x7fffffff) break;  // optimal
+            p = bid;
+            if (ln == q) u = 0.0;
+            fresh = false;
         }
-        wave_argmin(best, bid);
-        if (bid == 0x7fffffff) break;  // optimal
-        const int p = bid;
         double dj, sp;
         gi_project_reg<NF>(C, Jr, p, x, dj, sp, rowbuf);
-        if (ln == q) u = 0.0;
         // ---- step 2
-        for (;;) {
-            if (iters >= max_iter) { status = ST_ITER_LIMIT; done = true; break; }
-            ++iters;
-            double dd = ln < nf ? dj * dj : 0.0;
-            double zn = (ln >= q && ln < nf) ? dj * dj : 0.0;
-            wave_sum2(dd, zn);
-            double z4[4] = {0.0, 0.0, 0.0, 0.0};
+        if (iters >= max_iter) { status = ST_ITER_LIMIT; break; }
+        ++iters;
+        double dd = ln < nf ? dj * dj : 0.0;
+        double zn = (ln >= q && ln < nf) ? dj * dj : 0.0;
+        wave_sum2(dd, zn);
+        if (ln < NF) colb[ln] = (ln >= q) ? dj : 0.0;  // d_j = 0 for j >= nf
+        wave_sync();
+        double z4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int j = 0; j < NF; ++j)
-            {
-                if (j >= q) z4[j & 3] += Jr[j] * readlane(dj, j);  // d_j = 0 for j >= nf
-                if ((j & 15) == 15) step_fence();
+        for (int j = 0; j < NF; ++j) {
+            z4[j & 3] += Jr[j] * colb[j];
+            if ((j & 7) == 7) step_fence();
+        }
+        const double z = (z4[0] + z4[1]) + (z4[2] + z4[3]);
+        // r = R^-1 d(0:q) (R in LDS)
+        double r = 0.0, val = dj;
+        for (int j = q - 1; j >= 0; --j) {
+            const double rj = readlane(val, j) / L.R[roff(j) + j];
+            if (ln == j) r = rj;
+            if (ln < j) val -= L.R[roff(j) + ln] * rj;
+        }
+        const double rmax = wave_max(ln < q ? fabs(r) : 0.0);
+        double t1 = INFINITY;
+        int kslot = 0x7fffffff;
+        if (ln < q && r > kRTol * rmax) { t1 = u / r; kslot = ln; }
+        wave_argmin(t1, kslot);
+        const bool dep = !(zn > kDepTol * dd);
+        const double t2 = dep ? INFINITY : -sp / zn;
+        const double t = t1 < t2 ? t1 : t2;
+        if (isinf(t)) { status = ST_INFEASIBLE; break; }
+        const double uq = readlane(u, q);
+        if (!isinf(t2)) {
+            if (ln < nf) { x += t * z; L.xs[ln] = x; }
+            fval += t * zn * (0.5 * t + uq);
+        }
+        if (ln < q) u -= t * r;
+        if (ln == q) u += t;
+        const bool add = !isinf(t2) && t2 <= t1;
+        if (add) {
+            // ---- add p: Givens chain on d from the bottom up to q+1.  The chain's running
+            //      norm is the suffix norm of d, so every rotation (c_j, s_j) comes from
+            //      suffix sums of squares in parallel, lane j owning rotation j:
+            //        acc_j = d_j if T_{j+1} == 0 else sqrt(T_j),  T_j = sum_{i>=j} d_i^2
+            //        rotation j mixes (j-1, j): c = d_{j-1}/sqrt(T_{j-1}),
+            //        s = acc_j/sqrt(T_{j-1}) (identity when acc_j == 0)
+            const double t0 = wave_suffix_sum(ln < nf ? dj * dj : 0.0);
+            if (ln < NF) { colb[ln] = t0; rot[ln] = dj; }
+            wave_sync();
+            const double tm1 = (ln >= 1 && ln <= NF) ? colb[ln - 1] : t0;
+            const double dm1 = (ln >= 1 && ln <= NF) ? rot[ln - 1] : 0.0;
+            const double tp1 = (ln + 1 < NF) ? colb[ln + 1] : 0.0;
+            wave_sync();
+            const double accl = (tp1 == 0.0) ? dj : sqrt(t0);
+            double cl = 1.0, sl = 0.0;
+            if (ln > q && ln < nf && accl != 0.0) {
+                const double ih = rsqrt_nr(tm1);
+                cl = dm1 * ih;
+                sl = accl * ih;
             }
-            const double z = (z4[0] + z4[1]) + (z4[2] + z4[3]);
-            // r = R^-1 d(0:q) (R in LDS)
-            double r = 0.0, val = dj;
-            for (int j = q - 1; j >= 0; --j) {
-                const double rj = readlane(val, j) / L.R[roff(j) + j];
-                if (ln == j) r = rj;
-                if (ln < j) val -= L.R[roff(j) + ln] * rj;
-            }
-            const double rmax = wave_max(ln < q ? fabs(r) : 0.0);
-            double t1 = INFINITY;
-            int kslot = 0x7fffffff;
-            if (ln < q && r > kRTol * rmax) { t1 = u / r; kslot = ln; }
-            wave_argmin(t1, kslot);
-            const bool dep = !(zn > kDepTol * dd);
-            const double t2 = dep ? INFINITY : -sp / zn;
-            const double t = t1 < t2 ? t1 : t2;
-            if (isinf(t)) { status = ST_INFEASIBLE; done = true; break; }
-            const double uq = readlane(u, q);
-            if (isinf(t2)) {
-                if (ln < q) u -= t * r;
-                if (ln == q) u += t;
-            } else {
-                if (ln < nf) { x += t * z; L.xs[ln] = x; }
-                fval += t * zn * (0.5 * t + uq);
-                if (ln < q) u -= t * r;
-                if (ln == q) u += t;
-                if (t2 <= t1) {
-                    // ---- add p: Givens chain on d from the bottom up to q+1, applied to the
-                    //      J columns held in registers.  The chain's running norm is the
-                    //      suffix norm of d, so every rotation (c_j, s_j) comes from suffix
-                    //      sums of squares in parallel, lane j owning rotation j:
-                    //        acc_j = d_j if T_{j+1} == 0 else sqrt(T_j),  T_j = sum_{i>=j} d_i^2
-                    //        rotation j mixes (j-1, j): hh = sqrt(T_{j-1}), c = d_{j-1}/hh,
-                    //        s = acc_j/hh (identity when acc_j == 0)
-                    double tm1 = 0.0, t0 = 0.0, tp1 = 0.0, dm1 = 0.0;
-#pragma unroll
-                    for (int i = NF - 1; i >= 0; --i) {
-                        const double di = readlane(dj, i);  // 0 beyond nf
-                        const double d2 = di * di;
-                        if (i >= ln - 1) tm1 += d2;
-                        if (i >= ln) t0 += d2;
-                        if (i >= ln + 1) tp1 += d2;
-                        if (i == ln - 1) dm1 = di;
-                        if ((i & 15) == 0) step_fence();
-                    }
-                    const double accl = (tp1 == 0.0) ? dj : sqrt(t0);
-                    double cl = 1.0, sl = 0.0;
-                    if (accl != 0.0) {
-                        const double ih = 1.0 / sqrt(tm1);
-                        cl = dm1 * ih;
-                        sl = accl * ih;
-                    }
-#pragma unroll
-                    for (int j = NF - 1; j >= 1; --j) {
-                        if (j > q && j < nf) {
-                            const double c = readlane(cl, j), s = readlane(sl, j);
-                            const double x0 = Jr[j - 1], x1 = Jr[j];
-                            Jr[j - 1] = c * x0 + s * x1;
-                            Jr[j] = -s * x0 + c * x1;
-                        }
-                        if ((j & 15) == 0) step_fence();
-                    }
-                    const double rqq = readlane(accl, q);
-                    if (ln < q) L.R[roff(q) + ln] = dj;
-                    if (ln == q) { L.R[roff(q) + q] = rqq; act = p; }
-                    if (ln == 0) L.st[p] = 2;
-                    ++q;
-                    wave_sync();
-                    break;
-                }
-            }
-            // ---- drop slot kslot
+            if (ln < NF) { rot[2 * ln] = cl; rot[2 * ln + 1] = sl; }
+            const double rqq = readlane(accl, q);
+            if (ln < q) L.R[roff(q) + ln] = dj;
+            if (ln == q) { L.R[roff(q) + q] = rqq; act = p; }
+            if (ln == 0) L.st[p] = 2;
+            ++q;
+            fresh = true;
+        } else {
+            // ---- drop slot kslot: shift u/act and the R columns left, then restore R to
+            //      triangular with Givens rotations whose (c, s) go to LDS for J
             const int k = kslot;
             const int dropped = readlane(act, k);
             if (ln == 0) L.st[dropped] = 1;
@@ -290,29 +292,52 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                 wave_sync();
             }
             --q;
-#pragma unroll
-            for (int j = 0; j < NF - 1; ++j) {
-                if (j >= k && j < q) {
-                    const double a = L.R[roff(j) + j], bb = L.R[roff(j) + j + 1];
-                    if (bb != 0.0) {
-                        const double hh = sqrt(a * a + bb * bb);
-                        const double ih = 1.0 / hh;
-                        const double c = a * ih, s = bb * ih;
-                        const int l = j + 1 + ln;
-                        double r0 = 0.0, r1 = 0.0;
-                        if (l < q) { r0 = L.R[roff(l) + j]; r1 = L.R[roff(l) + j + 1]; }
-                        wave_sync();
-                        if (l < q) { L.R[roff(l) + j] = c * r0 + s * r1; L.R[roff(l) + j + 1] = -s * r0 + c * r1; }
-                        if (ln == 0) { L.R[roff(j) + j] = hh; L.R[roff(j) + j + 1] = 0.0; }
-                        wave_sync();
-                        const double x0 = Jr[j], x1 = Jr[j + 1];
-                        Jr[j] = c * x0 + s * x1;
-                        Jr[j + 1] = -s * x0 + c * x1;
+            if (ln < NF) { rot[2 * ln] = 1.0; rot[2 * ln + 1] = 0.0; }
+            wave_sync();
+            for (int j = k; j < q; ++j) {
+                const double a = L.R[roff(j) + j], bb = L.R[roff(j) + j + 1];
+                if (bb != 0.0) {
+                    const double hh = sqrt(a * a + bb * bb);
+                    const double ih = 1.0 / hh;
+                    const double c = a * ih, s_ = bb * ih;
+                    const int l = j + 1 + ln;
+                    double r0 = 0.0, r1 = 0.0;
+                    if (l < q) { r0 = L.R[roff(l) + j]; r1 = L.R[roff(l) + j + 1]; }
+                    wave_sync();
+                    if (l < q) { L.R[roff(l) + j] = c * r0 + s_ * r1; L.R[roff(l) + j + 1] = -s_ * r0 + c * r1; }
+                    if (ln == 0) {
+                        L.R[roff(j) + j] = hh;
+                        L.R[roff(j) + j + 1] = 0.0;
+                        rot[2 * j] = c;
+                        rot[2 * j + 1] = s_;
                     }
+                    wave_sync();
                 }
             }
-            gi_project_reg<NF>(C, Jr, p, x, dj, sp, rowbuf);
         }
+        wave_sync();
+        // ---- the pass's rotations of J: add -> pairs (j-1, j) for j = NF-1 .. 1,
+        //      drop -> pairs (j, j+1) for j = 0 .. NF-2; identity where (c, s) = (1, 0)
+        if (add) {
+#pragma unroll
+            for (int j = NF - 1; j >= 1; --j) {
+                const double c = rot[2 * j], s_ = rot[2 * j + 1];
+                const double x0 = Jr[j - 1], x1 = Jr[j];
+                Jr[j - 1] = c * x0 + s_ * x1;
+                Jr[j] = -s_ * x0 + c * x1;
+                if ((j & 7) == 0) step_fence();
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < NF - 1; ++j) {
+                const double c = rot[2 * j], s_ = rot[2 * j + 1];
+                const double x0 = Jr[j], x1 = Jr[j + 1];
+                Jr[j] = c * x0 + s_ * x1;
+                Jr[j + 1] = -s_ * x0 + c * x1;
+                if ((j & 7) == 7) step_fence();
+            }
+        }
+        wave_sync();
     }
     MPCQP_STAMP(C.stamps, 8, tst); MPCQP_CUT(C.cut, 7);
     C.status = status;

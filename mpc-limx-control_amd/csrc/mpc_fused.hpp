@@ -58,8 +58,8 @@ struct MpcLayout {
     static constexpr int oAx = oUV + (N + 1) * 2 * NU;   // A x0 (NX), A^2 x0 (NX)
     static constexpr int oR = oAx + 2 * NX;              // R factor (packed / NF x LD)
     static constexpr int oJ = oR + NR;                   // J (LDS solver only)
-    static constexpr int oRow = oJ + (REG ? 0 : NF * LD);// row broadcast buffer (NF)
-    static constexpr int oG = oRow + NF;                 // g (LDS solver)
+    static constexpr int oRow = oJ + (REG ? 0 : NF * LD);// broadcast buffers (4 NF)
+    static constexpr int oG = oRow + 4 * NF;             // g (LDS solver)
     static constexpr int oXS = oG + NF;
     static constexpr int oXF = oXS + NF;                 // xfull (NV)
     static constexpr int oMisc = oXF + NV;               // rowfix / ys slot
@@ -69,6 +69,7 @@ struct MpcLayout {
     static constexpr size_t bytes =
         sizeof(double) * nDoubles + sizeof(int) * (NF + NV) + ((MT + 15) & ~15);
     static constexpr size_t lds_bytes = (bytes + 15) & ~(size_t)15;
+    static_assert(oRow % 2 == 0, "broadcast buffers must be 16-byte aligned");
 };
 
 // sum over m in [m0, m1] of 1, beta_i, beta_j, beta_i beta_j; beta_x = m - 1 - k_x + 1/2

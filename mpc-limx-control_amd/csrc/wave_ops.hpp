@@ -46,6 +46,28 @@ __device__ __forceinline__ double dpp(double v) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+// DPP move that reads 0 where the source lane is outside the row
+template <int CTRL>
+__device__ __forceinline__ double dpp_z(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// inclusive suffix sum over the wave: lane l gets sum_{i >= l} v_i.  row_shl 1,2,4,8 scans
+// each 16-lane row; the rows after this one are added from their totals (lanes 16, 32, 48).
+__device__ __forceinline__ double wave_suffix_sum(double v) {
+    v += dpp_z<0x101>(v);
+    v += dpp_z<0x102>(v);
+    v += dpp_z<0x104>(v);
+    v += dpp_z<0x108>(v);
+    const double r1 = readlane(v, 16), r2 = readlane(v, 32), r3 = readlane(v, 48);
+    const int row = lane() >> 4;
+    const double add = row == 0 ? (r1 + r2) + r3 : row == 1 ? r2 + r3 : row == 2 ? r3 : 0.0;
+    return v + add;
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
     v += dpp<kDppXor1>(v);
     v += dpp<kDppXor2>(v);
