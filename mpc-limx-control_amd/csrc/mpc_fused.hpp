@@ -65,7 +65,8 @@ struct MpcLayout {
     static constexpr int oMisc = oXF + NV;               // rowfix / ys slot
     static constexpr int oXr = oMisc + 2;                // xref (NX x (N+1)) prefetch
     static constexpr int oX0v = oXr + NX * (N + 1);      // x0 prefetch (NX)
-    static constexpr int nDoubles = oX0v + NX + 1;
+    static constexpr int oRm = oX0v + NX + 1;            // R (NU x NU) copy
+    static constexpr int nDoubles = oRm + NU * NU;
     static constexpr size_t bytes =
         sizeof(double) * nDoubles + sizeof(int) * (NF + NV) + ((MT + 15) & ~15);
     static constexpr size_t lds_bytes = (bytes + 15) & ~(size_t)15;
@@ -78,7 +79,7 @@ __device__ __forceinline__ void beta_sums(int m0, int m1, int ki, int kj, double
     if (m1 < m0) { c = si = sj = sij = 0.0; return; }
     const double n = (double)(m1 - m0 + 1);
     const double s1 = 0.5 * (double)(m0 + m1) * n;  // sum m
-    auto S2 = [](int t) { return (double)t * (t + 1) * (2 * t + 1) / 6.0; };
+    auto S2 = [](int t) { return (double)(t * (t + 1) * (2 * t + 1) / 6); };  // exact in int
     const double s2 = S2(m1) - S2(m0 - 1);           // sum m^2
     const double oi = (double)ki + 0.5, oj = (double)kj + 0.5;
     c = n;
@@ -128,17 +129,27 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     C.L.pos = ip + NF;
     C.L.st = reinterpret_cast<unsigned char *>(ip + NF + NV);
 
-    // ---- per-instance inputs: one coalesced sweep into LDS
+    // ---- per-instance inputs: all global loads issued back to back (one HBM round trip),
+    //      then parked in LDS
     double *xr = D + Lay::oXr, *x0g = D + Lay::oX0v;
+    double lin[8];
     {
-        const double *xrg = a.xref + (size_t)b * NX * (N + 1);
-        for (int e = ln; e < NX * (N + 1); e += kWave) xr[e] = xrg[e];
-        if (ln < NX) x0g[ln] = a.x0[(size_t)b * NX + ln];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) lin[i] = a.lin[(size_t)b * 8 + i];
+        constexpr int NXR = NX * (N + 1), RX = (NXR + kWave - 1) / kWave;
+        const double *xrg = a.xref + (size_t)b * NXR;
+        double v[RX];
+#pragma unroll
+        for (int r = 0; r < RX; ++r) v[r] = (ln + r * kWave < NXR) ? xrg[ln + r * kWave] : 0.0;
+        const double x0l = (ln < NX) ? a.x0[(size_t)b * NX + ln] : 0.0;
+        const double rml = (ln < NU * NU) ? a.rmat[ln] : 0.0;
+#pragma unroll
+        for (int r = 0; r < RX; ++r)
+            if (ln + r * kWave < NXR) xr[ln + r * kWave] = v[r];
+        if (ln < NX) x0g[ln] = x0l;
+        if (ln < NU * NU) D[Lay::oRm + ln] = rml;
     }
     // ---- model: X0 = Bc Ts, X1 = (Ac Ts)(Bc Ts); A x0, A^2 x0
-    double lin[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) lin[i] = a.lin[(size_t)b * 8 + i];
     wave_sync();
     double Iwi[9];
     double cy = 1.0, sy = 0.0;
@@ -246,7 +257,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
         const int o = cj * NU + ci, nn = NU * NU;
         double v = c * S[0 * nn + o] + sj * S[1 * nn + o] + si * S[2 * nn + o] + sij * S[3 * nn + o];
         v += S[4 * nn + o] + bj * S[5 * nn + o] + bi * S[6 * nn + o] + bi * bj * S[7 * nn + o];
-        if (ki == kj) v += a.rmat[cj * NU + ci];
+        if (ki == kj) v += D[Lay::oRm + cj * NU + ci];
         return 2.0 * v;
     };
     double gp = 0.0;
@@ -267,12 +278,14 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
         double *Hb = C.L.R;
         if (ok) {
             const int E = nf * (nf + 1) / 2;
+            // row-major packed e = lrow(p) + q; lane ln starts at e = ln (p < 11 since
+            // lrow(11) = 66 > 63) and steps by 64
+            int p = 0, q = ln;
+            while (q > p) { q -= p + 1; ++p; }
             for (int e = ln; e < E; e += kWave) {
-                int p = (int)((sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
-                while (p * (p + 1) / 2 > e) --p;
-                while ((p + 1) * (p + 2) / 2 <= e) ++p;
-                const int q = e - p * (p + 1) / 2;
-                Hb[e] = H_entry(C.L.fid[p], C.L.fid[q]);  // row-major packed: e = lrow(p) + q
+                Hb[e] = H_entry(C.L.fid[p], C.L.fid[q]);
+                q += kWave;
+                while (q > p) { q -= p + 1; ++p; }
             }
         }
         wave_sync();
