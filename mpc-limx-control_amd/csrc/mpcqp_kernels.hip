@@ -212,7 +212,7 @@ __global__ void __launch_bounds__(64) k_condense_solve(FastArgs a) {
 }
 
 template <int NU, int N, int MODEL, bool FRIC, int NF>
-__global__ void __launch_bounds__(64, (NF <= 32 ? 3 : 1)) k_mpc(MpcArgs a) {
+__global__ void __launch_bounds__(64, (NF <= 32 ? 3 : 2)) k_mpc(MpcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_m[];
     if ((int)blockIdx.x >= a.B) return;
     fast_mpc<NU, N, MODEL, FRIC, NF>(a, smem_m);
