@@ -223,7 +223,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
             double acc = 0.0;
 #pragma unroll
             for (int l = 0; l < NX; ++l) acc += Xr[ci * NX + l] * w[l] * Xs[cj * NX + l];
-            S[rs * NU * NU + e] = acc;
+            S[e * 8 + rs] = acc;  // [o = cj NU + ci][rs]: one entry's 8 terms contiguous
         }
     }
     // ---- u_m(c) = X0[:,c]' W_m e_m, v_m(c) = X1[:,c]' W_m e_m, m = 1..N
@@ -254,9 +254,9 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
         double c, si, sj, sij;
         beta_sums(kk + 1, N - 1, ki, kj, c, si, sj, sij);
         const double bi = (double)(N - 1 - ki) + 0.5, bj = (double)(N - 1 - kj) + 0.5;
-        const int o = cj * NU + ci, nn = NU * NU;
-        double v = c * S[0 * nn + o] + sj * S[1 * nn + o] + si * S[2 * nn + o] + sij * S[3 * nn + o];
-        v += S[4 * nn + o] + bj * S[5 * nn + o] + bi * S[6 * nn + o] + bi * bj * S[7 * nn + o];
+        const double *So = S + (cj * NU + ci) * 8;
+        double v = c * So[0] + sj * So[1] + si * So[2] + sij * So[3];
+        v += So[4] + bj * So[5] + bi * So[6] + bi * bj * So[7];
         if (ki == kj) v += D[Lay::oRm + cj * NU + ci];
         return 2.0 * v;
     };
@@ -277,15 +277,38 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
         // the identity so the register factorization runs without predicates
         double *Hb = C.L.R;
         if (ok) {
-            const int E = nf * (nf + 1) / 2;
-            // row-major packed e = lrow(p) + q; lane ln starts at e = ln (p < 11 since
-            // lrow(11) = 66 > 63) and steps by 64
-            int p = 0, q = ln;
-            while (q > p) { q -= p + 1; ++p; }
-            for (int e = ln; e < E; e += kWave) {
-                Hb[e] = H_entry(C.L.fid[p], C.L.fid[q]);
-                q += kWave;
-                while (q > p) { q -= p + 1; ++p; }
+            // one lane per block pair (ki >= kj), row-major packed over the N(N+1)/2 pairs:
+            // the beta sums are per block, then the lane walks its block's free entries
+            constexpr int NPAIR = N * (N + 1) / 2;
+            const int *pos = C.L.pos;
+            int ki = 0, kj = ln;
+            while (kj > ki) { kj -= ki + 1; ++ki; }
+            for (int bp = ln; bp < NPAIR; bp += kWave) {
+                double c, si, sj, sij;
+                beta_sums(ki + 1, N - 1, ki, kj, c, si, sj, sij);
+                const double bi = (double)(N - 1 - ki) + 0.5, bj = (double)(N - 1 - kj) + 0.5;
+                const double bij = bi * bj;
+                int mi = 0, mj = 0;
+#pragma unroll
+                for (int cc = 0; cc < NU; ++cc) {
+                    mi |= (pos[ki * NU + cc] >= 0) << cc;
+                    mj |= (pos[kj * NU + cc] >= 0) << cc;
+                }
+                for (int ri = mi; ri; ri &= ri - 1) {
+                    const int ci = __builtin_ctz(ri), pp = pos[ki * NU + ci];
+                    for (int rj = mj; rj; rj &= rj - 1) {
+                        const int cj = __builtin_ctz(rj), qq = pos[kj * NU + cj];
+                        if (pp >= qq) {
+                            const double *So = S + (cj * NU + ci) * 8;
+                            double v = c * So[0] + sj * So[1] + si * So[2] + sij * So[3];
+                            v += So[4] + bj * So[5] + bi * So[6] + bij * So[7];
+                            if (ki == kj) v += D[Lay::oRm + cj * NU + ci];
+                            Hb[lrow(pp) + qq] = 2.0 * v;
+                        }
+                    }
+                }
+                kj += kWave;
+                while (kj > ki) { kj -= ki + 1; ++ki; }
             }
         }
         wave_sync();
