@@ -109,12 +109,13 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         // ---- Cholesky, right-looking; lane i owns row i.  h is padded with the identity
         //      beyond nf (and g with 0), so every step runs unpredicated (upper-triangle junk
         //      is never read).  The forward solve L t = g runs in the same sweep.
-        bool bad = false;
+        //      Look-ahead: lane k+1's own L(k+1,k) gives the next pivot without waiting for
+        //      the LDS broadcast, so the pivot's rsqrt overlaps the step's bulk update.
+        double piv = readlane(h[0], 0);
+        bool bad = !(piv > 0.0);
+        double ik = rsqrt_nr(piv);
 #pragma unroll
         for (int k = 0; k < NF; ++k) {
-            const double piv = readlane(h[k], k);
-            bad |= !(piv > 0.0);
-            const double ik = rsqrt_nr(piv);
             const double lkk = piv * ik;
             const double lik = (ln == k) ? lkk : h[k] * ik;
             const double tk = readlane(gv, k) * ik;
@@ -122,6 +123,12 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             gv = (ln == k) ? tk : ((ln > k) ? gv - lik * tk : gv);
             dinv = (ln == k) ? ik : dinv;
             if (ln > k && ln < NF) colb[ln] = lik;  // column k of L, broadcast through LDS
+            double pivn = 1.0, ikn = 1.0;
+            if (k + 1 < NF) {
+                pivn = readlane(h[k + 1 < NF ? k + 1 : k] - lik * lik, k + 1);
+                bad |= !(pivn > 0.0);
+                ikn = rsqrt_nr(pivn);
+            }
             wave_sync();
 #pragma unroll
             for (int j = 0; j < NF; ++j)
@@ -134,6 +141,10 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                 if (j >= k) pin(h[j]);  // step k's updates happen in step k
             pin(gv);
             pin(dinv);
+            piv = pivn;
+            ik = ikn;
+            pin(piv);
+            pin(ik);
             step_fence();
         }
         if (bad) status = ST_NOT_PD;
