@@ -44,14 +44,19 @@ __device__ __forceinline__ double srbm_entry(int i, int j, const double *lin, do
     }
     const int u = j - 13, ft = u / 3, c = u % 3;
     if (i >= 6 && i < 9) {  // Iw^-1 [r_ft]x, column c
-        const double *r = lin + 1 + 3 * ft;
+        // selects instead of indexing, so a lane-varying i or j never forces the small
+        // arrays into scratch
+        const double r0 = ft ? lin[4] : lin[1], r1 = ft ? lin[5] : lin[2], r2 = ft ? lin[6] : lin[3];
         // column c of [r]x
         double x0, x1, x2;
-        if (c == 0) { x0 = 0.0; x1 = r[2]; x2 = -r[1]; }
-        else if (c == 1) { x0 = -r[2]; x1 = 0.0; x2 = r[0]; }
-        else { x0 = r[1]; x1 = -r[0]; x2 = 0.0; }
+        if (c == 0) { x0 = 0.0; x1 = r2; x2 = -r1; }
+        else if (c == 1) { x0 = -r2; x1 = 0.0; x2 = r0; }
+        else { x0 = r1; x1 = -r0; x2 = 0.0; }
         const int ii = i - 6;
-        return Iwi[ii] * x0 + Iwi[3 + ii] * x1 + Iwi[6 + ii] * x2;
+        const double w0 = ii == 0 ? Iwi[0] : (ii == 1 ? Iwi[1] : Iwi[2]);
+        const double w1 = ii == 0 ? Iwi[3] : (ii == 1 ? Iwi[4] : Iwi[5]);
+        const double w2 = ii == 0 ? Iwi[6] : (ii == 1 ? Iwi[7] : Iwi[8]);
+        return w0 * x0 + w1 * x1 + w2 * x2;
     }
     if (i >= 9 && i < 12) return (i - 9 == c) ? 1.0 / mass : 0.0;
     return 0.0;

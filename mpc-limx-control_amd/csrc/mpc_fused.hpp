@@ -49,7 +49,8 @@ struct MpcLayout {
     static constexpr int NFRIC = FRIC ? 4 * N * 2 : 0;
     static constexpr int MT = 2 * NF + NFRIC;
     static constexpr bool REG = NF <= 64;
-    static constexpr int NR = REG ? RegPack<NF>::doubles : NF * LD;
+    static constexpr int NR0 = REG ? RegPack<NF>::doubles : NF * LD;
+    static constexpr int NR = NR0 > NX * (NX + NU) ? NR0 : NX * (NX + NU);  // also model scratch
     // doubles
     static constexpr int oX0 = 0;                        // B  (NX x NU)
     static constexpr int oX1 = oX0 + NX * NU;            // AB (NX x NU)
@@ -151,6 +152,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     }
     // ---- model: X0 = Bc Ts, X1 = (Ac Ts)(Bc Ts); A x0, A^2 x0
     wave_sync();
+    MPCQP_CUT(a.cut, 11);
     double Iwi[9];
     double cy = 1.0, sy = 0.0;
     if (MODEL == 0) {
@@ -176,19 +178,25 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
                 Iwi[j * 3 + i] = s;
             }
     }
+    MPCQP_CUT(a.cut, 12);
     auto entry = [&](int i, int j) -> double {  // [Ac | Bc](i, j)
         return MODEL == 0 ? srbm_entry(i, j, lin, cy, sy, Iwi, a.mass)
                           : literal_entry(i, j, lin, a.mass);
     };
     const double Ts = a.Ts;
-    for (int e = ln; e < NX * NU; e += kWave) {
-        const int i = e % NX, c = e / NX;
-        X0[e] = entry(i, NX + c) * Ts;
+    // [Ac | Bc] into LDS once, lane i writing row i with compile-time columns (the R space is
+    // free until H_FF is built there); the products then read it
+    double *T = C.L.R;
+    if (ln < NX) {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) T[j * NX + ln] = entry(ln, j);
     }
+    wave_sync();
+    for (int e = ln; e < NX * NU; e += kWave) X0[e] = T[NX * NX + e] * Ts;
     if (ln < NX) {
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < NX; ++k) s += entry(ln, k) * x0g[k];
+        for (int k = 0; k < NX; ++k) s += T[k * NX + ln] * x0g[k];
         Ax[ln] = s * Ts;
     }
     wave_sync();
@@ -196,15 +204,17 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
         const int i = e % NX, c = e / NX;
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < NX; ++k) s += entry(i, k) * X0[c * NX + k];
+        for (int k = 0; k < NX; ++k) s += T[k * NX + i] * X0[c * NX + k];
         X1[e] = s * Ts;
     }
     if (ln < NX) {
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k < NX; ++k) s += entry(ln, k) * Ax[k];
+        for (int k = 0; k < NX; ++k) s += T[k * NX + ln] * Ax[k];
         A2x[ln] = s * Ts;
     }
+    wave_sync();
+    MPCQP_CUT(a.cut, 13);
     gi_setup(C);  // free map + constraint states
     if (C.nf > a.max_free) C.status = ST_BAD_DIMS;
     wave_sync();

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--configs", default="B,C,L")
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--cuts", default="", help="comma list of extra cut ids to time (e.g. 11,12,13)")
     args = ap.parse_args()
     import mpcqp
     from mpcqp.engine import BatchEngine
@@ -37,7 +38,8 @@ def main():
         eng.enable_timing(True)
         prev = 0.0
         print(f"config {cfg}: batch {args.batch}, fast path {eng.fast_path}")
-        for cut, name in CUTS:
+        cuts = CUTS if not args.cuts else [(int(c), f"cut {c}") for c in args.cuts.split(",")]
+        for cut, name in cuts:
             os.environ["MPCQP_CUT"] = str(cut)
             ts = []
             for r in range(args.reps + 2):
