@@ -32,6 +32,11 @@
  * mpcqp_batch_condense_solve      QPSolver::buildQPParams + QPSolver::solveQP, batched, fused
  *                                 (H never leaves the chip)
  * mpcqp_batch_select_min          (new) per-rank min-cost key for the multi-GPU selection
+ * mpcqp_batch_solve_gait          mpcQP::mpcQP xref (include/mpcQP.h:74-97) + MPC::calculateGait
+ *                                 (include/MPCController.h:61-75) on device, then the fused step
+ * mpcqp_batch_select_state        (new) best gait candidate per state
+ * mpcqp_batch_plant_srbm          QPSolver::updateState (src/QPSolver.cpp:108-111), SRBM, batched
+ * mpcqp_rollout                   the closed loop of src/qpSolver_test.cpp:38-90, batched
  */
 #ifndef MPCQP_H
 #define MPCQP_H
@@ -165,6 +170,34 @@ int mpcqp_batch_solve_host(mpcqp_ctx *ctx, int B, const double *x0, const double
  * reduces keys across ranks with one MIN all-reduce (RCCL). */
 int mpcqp_batch_select_min(mpcqp_ctx *ctx, int B, const double *cost, const int *status,
                            int64_t index_base, int64_t *key);
+
+/* ---- device-generated inputs, per-state selection and the closed loop ---- *
+ * SRBM fast-path contexts only.  S states x C gait candidates, instance b = s*C + c.
+ *   state [S][13]   [rpy, p, omega, v, g]                      (include/mpcQP.h:66-71)
+ *   feet  [S][6]    r_L, r_R: foot minus CoM, world frame
+ *   cmd   [S][2]    yaw rate, forward speed of the reference  (include/mpcQP.h:75-76)
+ *   phase [S*C]     gait phase of each candidate at horizon step 0 (s)
+ * The kernel builds x0 = state, xref as mpcQP::mpcQP does (include/mpcQP.h:74-97), lin =
+ * {yaw, r_L, r_R} and the contact mask of MPC::calculateGait (include/MPCController.h:61-75)
+ * on chip, then runs the same fused step as mpcqp_batch_solve. */
+int mpcqp_batch_solve_gait(mpcqp_ctx *ctx, int S, int C, const double *state, const double *feet,
+                           const double *cmd, const double *phase, float swing, float stance,
+                           double *U, double *cost, int *status, int *iters);
+/* best candidate of each state (status OK, fp32 cost, lowest index; best = -1 if none):
+ * best [S], best_cost [S] (nullable), Ubest [S][nu*N] (nullable).  C <= 64. */
+int mpcqp_batch_select_state(mpcqp_ctx *ctx, int S, int C, const double *cost, const int *status,
+                             const double *U, int *best, double *best_cost, double *Ubest);
+/* plant step with each state's chosen first-step forces: state <- Ad state + Bd u (exact ZOH of
+ * the SRBM at the current state, QPSolver::updateState, src/QPSolver.cpp:108-111), feet moved
+ * with the CoM (stance feet fixed in the world), phase[S*C] += Ts. */
+int mpcqp_batch_plant_srbm(mpcqp_ctx *ctx, int S, int C, double *state, double *feet,
+                           double *phase, const int *best, const double *Ubest);
+/* K closed-loop ticks of solve_gait -> select_state -> plant_srbm on the ctx stream (the
+ * qp_test / mpc_test loops, src/qpSolver_test.cpp:38-90, at batch scale).  traj [K][S][13] and
+ * choice [K][S] (nullable) receive the state after each tick and the chosen candidate. */
+int mpcqp_rollout(mpcqp_ctx *ctx, int S, int C, int K, double *state, double *feet,
+                  const double *cmd, double *phase, float swing, float stance, double *traj,
+                  int *choice);
 
 /* duration of the last stage-1 (which = 0: discretize / generic condense) or stage-2
  * (which = 1: condense_solve / generic solve) kernel, HIP events on the ctx stream (ms; -1 if

@@ -62,6 +62,32 @@ __device__ __forceinline__ double srbm_entry(int i, int j, const double *lin, do
     return 0.0;
 }
 
+// Rz(yaw) and the world-frame inverse inertia Iw^-1 = Rz Ib^-1 Rz' (column-major)
+__device__ __forceinline__ void srbm_rot_inertia(double yaw, const double *Ibinv, double &cy,
+                                                 double &sy, double *Iwi) {
+    sincos(yaw, &sy, &cy);
+    const double Rz[9] = {cy, sy, 0.0, -sy, cy, 0.0, 0.0, 0.0, 1.0};
+    double Tm[9];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            double s = 0.0;
+#pragma unroll
+            for (int l = 0; l < 3; ++l) s += Rz[l * 3 + i] * Ibinv[j * 3 + l];
+            Tm[j * 3 + i] = s;
+        }
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            double s = 0.0;
+#pragma unroll
+            for (int l = 0; l < 3; ++l) s += Tm[l * 3 + i] * Rz[l * 3 + j];
+            Iwi[j * 3 + i] = s;
+        }
+}
+
 // reference mpcQP::buildSystemModel, include/mpcQP.h:154-181 (lin = {dx, dy, dz})
 __device__ __forceinline__ double literal_entry(int i, int j, const double *lin, double mass) {
     const double dx = lin[0], dy = lin[1], dz = lin[2];

@@ -41,7 +41,36 @@ struct MpcArgs {
     int *status, *iters;
     unsigned long long *stamps;
     int cut;  // diagnostic cuts build only
+    // device-generated inputs (GEN kernels): instance b = state b / cands,
+    // candidate b % cands
+    const double *state;  // [S][13]  [rpy, p, omega, v, g]
+    const double *feet;   // [S][6]   r_L, r_R (foot minus CoM, world frame)
+    const double *cmd;    // [S][2]   yaw rate, forward speed (include/mpcQP.h:75-76)
+    const double *phase;  // [S * cands] gait phase of each candidate at step 0 (s)
+    int cands;
+    float swing, stance;  // MPCParam::swing_time / stance_time (float, include/MPCParam.h:48-49)
 };
+
+// Gait contact mask of one horizon: MPC::calculateGait (include/MPCController.h:61-75)
+// evaluated at phase0 + k Ts for k = 0..N-1 (lane k, exact fmod as the host's math.fmod);
+// bit 2k = left foot in contact, 2k+1 = right.  Wave-uniform result.
+__device__ __forceinline__ uint64_t spread_even(uint64_t x) {  // bit i -> bit 2i (i < 32)
+    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    x = (x | (x << 1)) & 0x5555555555555555ull;
+    return x;
+}
+__device__ __forceinline__ uint64_t gait_mask_wave(int N, double Ts, double phase0, float swing,
+                                                   float stance) {
+    const double cycle = (double)(swing + stance), sw = (double)swing;
+    const int ln = lane();
+    const double ph = fmod(phase0 + (double)ln * Ts, cycle);
+    const uint64_t right = __ballot(ln < N && ph < sw) & 0xffffffffull;
+    const uint64_t left = __ballot(ln < N && !(ph < sw)) & 0xffffffffull;
+    return spread_even(left) | (spread_even(right) << 1);
+}
 
 template <int NU, int N, bool FRIC, int NF>
 struct MpcLayout {
@@ -89,8 +118,9 @@ __device__ __forceinline__ void beta_sums(int m0, int m1, int ki, int kj, double
     sij = s2 - (oi + oj) * s1 + oi * oj * n;
 }
 
-template <int NU, int N, int MODEL, bool FRIC, int NF>
+template <int NU, int N, int MODEL, bool FRIC, int NF, bool GEN = false>
 __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) {
+    static_assert(!GEN || MODEL == 0, "generated inputs are defined for the SRBM model");
     using Lay = MpcLayout<NU, N, FRIC, NF>;
     constexpr int NX = 13, NS = NX + NU, NV = Lay::NV, LD = Lay::LD;
     const int b = blockIdx.x, ln = lane();
@@ -107,7 +137,9 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     P.model = MODEL; P.nu = NU; P.N = N; P.nfeet = 2;
     P.fz_min = a.fz_min; P.fz_max = a.fz_max; P.fxy_max = a.fxy_max;
     P.u_min = a.u_min; P.u_max = a.u_max;
-    P.contact = (MODEL == 0) ? a.contact[b] : 0ull;
+    const int st_ = GEN ? b / a.cands : b;  // state row of this instance (GEN)
+    P.contact = (MODEL != 0) ? 0ull
+              : GEN ? gait_mask_wave(N, a.Ts, a.phase[b], a.swing, a.stance) : a.contact[b];
     P.friction = FRIC ? 1 : 0;
     P.mu = a.mu;
     P.mA = 0; P.A = nullptr; P.a_colmajor = 0; P.lbA = nullptr; P.ubA = nullptr;
@@ -134,7 +166,31 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     //      then parked in LDS
     double *xr = D + Lay::oXr, *x0g = D + Lay::oX0v;
     double lin[8];
-    {
+    if constexpr (GEN) {
+        // x0 = the state; xref as mpcQP::mpcQP builds it (include/mpcQP.h:74-97) from the
+        // state and the (yaw rate, forward speed) command; lin = {yaw, r_L, r_R}
+        const double st = (ln < NX) ? a.state[(size_t)st_ * NX + ln] : 0.0;
+        const double wz = a.cmd[(size_t)st_ * 2], vx = a.cmd[(size_t)st_ * 2 + 1];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) lin[1 + i] = a.feet[(size_t)st_ * 6 + i];
+        lin[7] = 0.0;
+        const double rml = (ln < NU * NU) ? a.rmat[ln] : 0.0;
+        if (ln < NX) x0g[ln] = st;
+        if (ln < NU * NU) D[Lay::oRm + ln] = rml;
+        lin[0] = readlane(st, 2);
+        if (ln < NX) {
+#pragma unroll
+            for (int i = 0; i <= N; ++i) {
+                const double t = (double)i * a.Ts;
+                double v = st;
+                if (ln == 2) v = st + t * wz;
+                if (ln == 3) v = st + t * vx;
+                if (ln == 9 && i > 0) v = vx;
+                if (ln == 12) v = -9.8;
+                xr[i * NX + ln] = v;
+            }
+        }
+    } else {
 #pragma unroll
         for (int i = 0; i < 8; ++i) lin[i] = a.lin[(size_t)b * 8 + i];
         constexpr int NXR = NX * (N + 1), RX = (NXR + kWave - 1) / kWave;
@@ -150,34 +206,13 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
         if (ln < NX) x0g[ln] = x0l;
         if (ln < NU * NU) D[Lay::oRm + ln] = rml;
     }
+    (void)st_;
     // ---- model: X0 = Bc Ts, X1 = (Ac Ts)(Bc Ts); A x0, A^2 x0
     wave_sync();
     MPCQP_CUT(a.cut, 11);
     double Iwi[9];
     double cy = 1.0, sy = 0.0;
-    if (MODEL == 0) {
-        sincos(lin[0], &sy, &cy);
-        const double Rz[9] = {cy, sy, 0.0, -sy, cy, 0.0, 0.0, 0.0, 1.0};
-        double Tm[9];
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                double s = 0.0;
-#pragma unroll
-                for (int l = 0; l < 3; ++l) s += Rz[l * 3 + i] * a.Ibinv[j * 3 + l];
-                Tm[j * 3 + i] = s;
-            }
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                double s = 0.0;
-#pragma unroll
-                for (int l = 0; l < 3; ++l) s += Tm[l * 3 + i] * Rz[l * 3 + j];
-                Iwi[j * 3 + i] = s;
-            }
-    }
+    if (MODEL == 0) srbm_rot_inertia(lin[0], a.Ibinv, cy, sy, Iwi);
     MPCQP_CUT(a.cut, 12);
     auto entry = [&](int i, int j) -> double {  // [Ac | Bc](i, j)
         return MODEL == 0 ? srbm_entry(i, j, lin, cy, sy, Iwi, a.mass)

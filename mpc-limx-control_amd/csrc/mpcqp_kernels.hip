@@ -196,6 +196,88 @@ __global__ void __launch_bounds__(64) k_plant(int nx, int nu, const double *Ad, 
     }
 }
 
+// best of each state's C gait candidates: (fp32 cost order bits, candidate) minimum, the same
+// rule as k_select_min; U row copied out.  One wave per state, C <= 64.
+__global__ void __launch_bounds__(64) k_select_state(int S, int C, int nV, const double *cost,
+                                                     const int *status, const double *U,
+                                                     int *best, double *best_cost, double *Ubest) {
+    const int s = blockIdx.x, c = threadIdx.x;
+    if (s >= S) return;
+    const size_t b = (size_t)s * C + c;
+    unsigned long long k = 0x7fffffffffffffffull;
+    if (c < C && status[b] == 0) k = (order_bits((float)cost[b]) << 31) | (unsigned)c;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long t = __shfl_xor(k, o, 64);
+        k = t < k ? t : k;
+    }
+    const int w = (k == 0x7fffffffffffffffull) ? -1 : (int)(k & 0x7fffffffull);
+    if (c == 0) {
+        best[s] = w;
+        if (best_cost) best_cost[s] = w >= 0 ? cost[(size_t)s * C + w] : INFINITY;
+    }
+    if (Ubest)
+        for (int i = c; i < nV; i += 64)
+            Ubest[(size_t)s * nV + i] = w >= 0 ? U[((size_t)s * C + w) * nV + i] : 0.0;
+}
+
+// SRBM plant step of each state with its chosen first-step forces:
+// x <- Ad x + Bd u = x + A x + A^2 x / 2 + B u + A B u / 2 (A = Ac Ts, B = Bc Ts, the exact ZOH
+// of the nilpotent model, as in k_mpc); stance feet stay fixed in the world, so both lever
+// arms move by -(p+ - p); every candidate's gait phase advances by Ts.
+struct PlantArgs {
+    int S, C, nV;
+    double Ts, mass;
+    double Ibinv[9];
+    double *state, *feet, *phase;
+    const double *Ubest;
+    const int *best;  // states with no solved candidate keep u = 0
+};
+
+__global__ void __launch_bounds__(64) k_plant_srbm(PlantArgs a) {
+    constexpr int NX = 13, NS = 19;
+    __shared__ double T[NX * NS], xs[NX], us[6], ax[NX], bu[NX];
+    const int s = blockIdx.x, ln = threadIdx.x;
+    if (s >= a.S) return;
+    double lin[8];
+    lin[0] = a.state[(size_t)s * NX + 2];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) lin[1 + i] = a.feet[(size_t)s * 6 + i];
+    lin[7] = 0.0;
+    double cy, sy, Iwi[9];
+    srbm_rot_inertia(lin[0], a.Ibinv, cy, sy, Iwi);
+    if (ln < NX) {
+#pragma unroll
+        for (int j = 0; j < NS; ++j) T[j * NX + ln] = srbm_entry(ln, j, lin, cy, sy, Iwi, a.mass);
+        xs[ln] = a.state[(size_t)s * NX + ln];
+    }
+    if (ln < 6) us[ln] = (a.best[s] >= 0) ? a.Ubest[(size_t)s * a.nV + ln] : 0.0;
+    __syncthreads();
+    if (ln < NX) {
+        double p = 0.0, q = 0.0;
+        for (int k = 0; k < NX; ++k) p += T[k * NX + ln] * xs[k];
+        for (int c = 0; c < 6; ++c) q += T[(NX + c) * NX + ln] * us[c];
+        ax[ln] = p * a.Ts;
+        bu[ln] = q * a.Ts;
+    }
+    __syncthreads();
+    double xn = 0.0;
+    if (ln < NX) {
+        double p = 0.0, q = 0.0;
+        for (int k = 0; k < NX; ++k) {
+            p += T[k * NX + ln] * ax[k];
+            q += T[k * NX + ln] * bu[k];
+        }
+        xn = xs[ln] + ax[ln] + 0.5 * (p * a.Ts) + bu[ln] + 0.5 * (q * a.Ts);
+        a.state[(size_t)s * NX + ln] = xn;
+    }
+    __syncthreads();
+    if (ln >= 3 && ln < 6) ax[ln] = xn - xs[ln];  // CoM displacement (reuse ax)
+    __syncthreads();
+    if (ln < 6) a.feet[(size_t)s * 6 + ln] -= ax[3 + ln % 3];
+    for (int c = ln; c < a.C; c += 64) a.phase[(size_t)s * a.C + c] += a.Ts;
+}
+
 // ------------------------------------------------------------------ fast path kernels
 template <int NX, int NU, int MODEL>
 __global__ void __launch_bounds__(64) k_discretize(FastArgs a) {
@@ -218,7 +300,17 @@ __global__ void __launch_bounds__(64, (NF <= 32 ? 3 : 2)) k_mpc(MpcArgs a) {
     fast_mpc<NU, N, MODEL, FRIC, NF>(a, smem_m);
 }
 
+// device-generated inputs: the same fused step, x0/xref/lin/contact
+// built on chip from per-state data, gait candidates and commands
+template <int NU, int N, int MODEL, bool FRIC, int NF>
+__global__ void __launch_bounds__(64, (NF <= 32 ? 3 : 2)) k_mpc_gen(MpcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_g[];
+    if ((int)blockIdx.x >= a.B) return;
+    fast_mpc<NU, N, MODEL, FRIC, NF, true>(a, smem_g);
+}
+
 struct FastKernels {
+    const void *mpc_gen = nullptr;
     const void *disc = nullptr, *cs = nullptr, *mpc = nullptr;
     size_t disc_lds = 0, cs_lds = 0, mpc_lds = 0;
     int nx = 0, nu = 0;
@@ -232,6 +324,7 @@ FastKernels make_fast() {
     k.disc_lds = sizeof(double) * disc_lds_doubles<NX, NU>();
     k.cs_lds = CSLayout<NX, NU, N, FRIC, NFMAX>::lds_bytes;
     k.mpc = (const void *)&k_mpc<NU, N, MODEL, FRIC, NFMAX>;
+    if constexpr (MODEL == 0) k.mpc_gen = (const void *)&k_mpc_gen<NU, N, MODEL, FRIC, NFMAX>;
     k.mpc_lds = MpcLayout<NU, N, FRIC, NFMAX>::lds_bytes;
     k.nx = NX;
     k.nu = NU;
@@ -337,6 +430,9 @@ struct mpcqp_ctx {
     // host-pointer entry point staging
     void *hbuf = nullptr;
     size_t hbuf_cap = 0;
+    // closed-loop rollout workspace
+    void *rbuf = nullptr;
+    size_t rbuf_cap = 0;
 };
 
 extern "C" {
@@ -639,6 +735,7 @@ int mpcqp_ctx_destroy(mpcqp_ctx *c) {
     hipFree(c->dAB);
     hipFree(c->dstamps);
     hipFree(c->hbuf);
+    hipFree(c->rbuf);
     hipFree(c->scratchH);
     hipFree(c->scratchF);
     if (c->ev_ok)
@@ -965,6 +1062,106 @@ int mpcqp_batch_solve_host(mpcqp_ctx *c, int B, const double *x0, const double *
         hipMemcpyAsync(iters, d_it, sizeof(int) * B, d2h, c->stream) != hipSuccess)
         return MPCQP_ERR_DEVICE;
     return hip_status(hipStreamSynchronize(c->stream));
+}
+
+int mpcqp_batch_solve_gait(mpcqp_ctx *c, int S, int C, const double *state, const double *feet,
+                           const double *cmd, const double *phase, float swing, float stance,
+                           double *U, double *cost, int *status, int *iters) {
+    if (!c || !state || !feet || !cmd || !phase || !U || !cost || !status || !iters || S < 0 ||
+        C <= 0)
+        return MPCQP_ERR_BAD_ARG;
+    if (!(swing > 0.0f) || !(stance >= 0.0f)) return MPCQP_ERR_BAD_ARG;
+    if (!c->fast || !c->fk.mpc_gen) return MPCQP_ERR_BAD_DIMS;  // SRBM fast-path models only
+    if ((long long)S * C > 0x7fffffffll) return MPCQP_ERR_BAD_DIMS;
+    const int B = S * C;
+    if (B == 0) return MPCQP_OK;
+    hipSetDevice(c->device);
+    MpcArgs a = mpc_args(c, B);
+    a.state = state;
+    a.feet = feet;
+    a.cmd = cmd;
+    a.phase = phase;
+    a.cands = C;
+    a.swing = swing;
+    a.stance = stance;
+    a.U = U;
+    a.cost = cost;
+    a.status = status;
+    a.iters = iters;
+    tbegin(c, 1);
+    const int rc = launch(c->fk.mpc_gen, B, c->fk.mpc_lds, c->stream, &a);
+    tend(c, 1);
+    return rc;
+}
+
+int mpcqp_batch_select_state(mpcqp_ctx *c, int S, int C, const double *cost, const int *status,
+                             const double *U, int *best, double *best_cost, double *Ubest) {
+    if (!c || !cost || !status || !best || S < 0 || C <= 0 || C > 64) return MPCQP_ERR_BAD_ARG;
+    if (Ubest && !U) return MPCQP_ERR_BAD_ARG;
+    if (S == 0) return MPCQP_OK;
+    hipSetDevice(c->device);
+    hipLaunchKernelGGL(k_select_state, dim3(S), dim3(64), 0, c->stream, S, C, c->m.nu * c->m.N,
+                       cost, status, U, best, best_cost, Ubest);
+    return hip_status(hipGetLastError());
+}
+
+int mpcqp_batch_plant_srbm(mpcqp_ctx *c, int S, int C, double *state, double *feet,
+                           double *phase, const int *best, const double *Ubest) {
+    if (!c || !state || !feet || !best || !Ubest || S < 0 || C < 0 || (C > 0 && !phase))
+        return MPCQP_ERR_BAD_ARG;
+    if (c->m.model != MPCQP_MODEL_SRBM || c->m.nx != 13 || c->m.nu != 6) return MPCQP_ERR_BAD_DIMS;
+    if (S == 0) return MPCQP_OK;
+    hipSetDevice(c->device);
+    PlantArgs a;
+    memset(&a, 0, sizeof(a));
+    a.S = S;
+    a.C = C;
+    a.nV = c->m.nu * c->m.N;
+    a.Ts = c->m.Ts;
+    a.mass = c->m.mass;
+    for (int i = 0; i < 9; ++i) a.Ibinv[i] = c->Ibinv[i];
+    a.state = state;
+    a.feet = feet;
+    a.phase = phase;
+    a.Ubest = Ubest;
+    a.best = best;
+    hipLaunchKernelGGL(k_plant_srbm, dim3(S), dim3(64), 0, c->stream, a);
+    return hip_status(hipGetLastError());
+}
+
+int mpcqp_rollout(mpcqp_ctx *c, int S, int C, int K, double *state, double *feet,
+                  const double *cmd, double *phase, float swing, float stance, double *traj,
+                  int *choice) {
+    if (!c || !state || !feet || !cmd || !phase || S < 0 || C <= 0 || C > 64 || K < 0)
+        return MPCQP_ERR_BAD_ARG;
+    if (!c->fast || !c->fk.mpc_gen) return MPCQP_ERR_BAD_DIMS;
+    if (S == 0 || K == 0) return MPCQP_OK;
+    hipSetDevice(c->device);
+    const size_t B = (size_t)S * C, nV = (size_t)c->m.nu * c->m.N;
+    const size_t bytes = sizeof(double) * (B * nV + B + S * nV + S) + sizeof(int) * (2 * B + S) + 64;
+    if (c->rbuf_cap < bytes) {
+        hipFree(c->rbuf);
+        c->rbuf = nullptr;
+        c->rbuf_cap = 0;
+        if (hipMalloc(&c->rbuf, bytes) != hipSuccess) return MPCQP_ERR_DEVICE;
+        c->rbuf_cap = bytes;
+    }
+    double *U = (double *)c->rbuf, *cost = U + B * nV, *Ub = cost + B, *bc = Ub + S * nV;
+    int *st = (int *)(bc + S), *it = st + B, *best = it + B;
+    for (int k = 0; k < K; ++k) {
+        int rc = mpcqp_batch_solve_gait(c, S, C, state, feet, cmd, phase, swing, stance, U, cost,
+                                        st, it);
+        if (!rc) rc = mpcqp_batch_select_state(c, S, C, cost, st, U, best, bc, Ub);
+        if (!rc) rc = mpcqp_batch_plant_srbm(c, S, C, state, feet, phase, best, Ub);
+        if (rc) return rc;
+        if (traj && hipMemcpyAsync(traj + (size_t)k * S * 13, state, sizeof(double) * S * 13,
+                                   hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
+            return MPCQP_ERR_DEVICE;
+        if (choice && hipMemcpyAsync(choice + (size_t)k * S, best, sizeof(int) * S,
+                                     hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
+            return MPCQP_ERR_DEVICE;
+    }
+    return MPCQP_OK;
 }
 
 int mpcqp_batch_select_min(mpcqp_ctx *c, int B, const double *cost, const int *status,

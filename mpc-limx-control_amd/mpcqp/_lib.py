@@ -27,6 +27,8 @@ EXPORTS = [
     "mpcqp_ctx_fast_path", "mpcqp_batch_discretize", "mpcqp_batch_condense_solve",
     "mpcqp_debug_phase_cycles", "mpcqp_batch_solve_host",
     "mpcqp_batch_select_min", "mpcqp_enable_timing", "mpcqp_last_kernel_ms",
+    "mpcqp_batch_solve_gait", "mpcqp_batch_select_state", "mpcqp_batch_plant_srbm",
+    "mpcqp_rollout",
     "mpcqp_status_string", "mpcqp_device_count",
 ]
 
@@ -78,6 +80,10 @@ def lib():
     L.mpcqp_batch_discretize.argtypes = [vp, i, vp, vp]
     L.mpcqp_batch_condense_solve.argtypes = [vp, i] + [vp] * 8
     L.mpcqp_batch_select_min.argtypes = [vp, i, vp, vp, C.c_int64, vp]
+    L.mpcqp_batch_solve_gait.argtypes = [vp, i, i] + [vp] * 4 + [C.c_float, C.c_float] + [vp] * 4
+    L.mpcqp_batch_select_state.argtypes = [vp, i, i] + [vp] * 6
+    L.mpcqp_batch_plant_srbm.argtypes = [vp, i, i] + [vp] * 5
+    L.mpcqp_rollout.argtypes = [vp, i, i, i] + [vp] * 4 + [C.c_float, C.c_float, vp, vp]
     L.mpcqp_enable_timing.argtypes = [vp, i]
     L.mpcqp_last_kernel_ms.argtypes = [vp, i]
     L.mpcqp_last_kernel_ms.restype = C.c_double

@@ -107,6 +107,55 @@ class BatchEngine:
             _ptr(d["contact"]), _ptr(d["U"]), _ptr(d["cost"]), _ptr(d["status"]),
             _ptr(d["iters"])))
 
+    # -- device-generated inputs and the closed loop ----------------
+    def upload_gait(self, g: dict):
+        """g: state [S,13], feet [S,6], cmd [S,2], phase [S,C] (numpy) -> device dict"""
+        t = self.torch
+        dev = f"cuda:{self.device}"
+        out = {k: t.from_numpy(np.ascontiguousarray(g[k], dtype=np.float64)).to(dev)
+               for k in ("state", "feet", "cmd", "phase")}
+        S, Cc = g["phase"].shape
+        B = S * Cc
+        out["U"] = t.zeros((B, self.nV), dtype=t.float64, device=dev)
+        out["cost"] = t.zeros(B, dtype=t.float64, device=dev)
+        out["status"] = t.zeros(B, dtype=t.int32, device=dev)
+        out["iters"] = t.zeros(B, dtype=t.int32, device=dev)
+        out["best"] = t.zeros(S, dtype=t.int32, device=dev)
+        out["best_cost"] = t.zeros(S, dtype=t.float64, device=dev)
+        out["Ubest"] = t.zeros((S, self.nV), dtype=t.float64, device=dev)
+        out["S"], out["C"], out["B"] = S, Cc, B
+        out["swing"] = float(g.get("swing", _model.SWING_TIME))
+        out["stance"] = float(g.get("stance", _model.STANCE_TIME))
+        return out
+
+    def solve_gait(self, g):
+        """x0 / xref / lin / contact generated on chip from the per-state data, then the step"""
+        check("mpcqp_batch_solve_gait", lib().mpcqp_batch_solve_gait(
+            self.ctx, g["S"], g["C"], _ptr(g["state"]), _ptr(g["feet"]), _ptr(g["cmd"]),
+            _ptr(g["phase"]), g["swing"], g["stance"], _ptr(g["U"]), _ptr(g["cost"]),
+            _ptr(g["status"]), _ptr(g["iters"])))
+
+    def select_state(self, g):
+        check("mpcqp_batch_select_state", lib().mpcqp_batch_select_state(
+            self.ctx, g["S"], g["C"], _ptr(g["cost"]), _ptr(g["status"]), _ptr(g["U"]),
+            _ptr(g["best"]), _ptr(g["best_cost"]), _ptr(g["Ubest"])))
+
+    def plant(self, g):
+        check("mpcqp_batch_plant_srbm", lib().mpcqp_batch_plant_srbm(
+            self.ctx, g["S"], g["C"], _ptr(g["state"]), _ptr(g["feet"]), _ptr(g["phase"]),
+            _ptr(g["best"]), _ptr(g["Ubest"])))
+
+    def rollout(self, g, K: int, record: bool = True):
+        """K closed-loop ticks on device; returns (traj [K,S,13], choice [K,S]) if record"""
+        t = self.torch
+        dev = g["state"].device
+        traj = t.empty((K, g["S"], 13), dtype=t.float64, device=dev) if record else None
+        choice = t.empty((K, g["S"]), dtype=t.int32, device=dev) if record else None
+        check("mpcqp_rollout", lib().mpcqp_rollout(
+            self.ctx, g["S"], g["C"], int(K), _ptr(g["state"]), _ptr(g["feet"]), _ptr(g["cmd"]),
+            _ptr(g["phase"]), g["swing"], g["stance"], _ptr(traj), _ptr(choice)))
+        return traj, choice
+
     def select_min(self, d, index_base: int = 0):
         check("mpcqp_batch_select_min", lib().mpcqp_batch_select_min(
             self.ctx, d["B"], _ptr(d["cost"]), _ptr(d["status"]), int(index_base),

@@ -97,3 +97,57 @@ def qp_harness_inputs(k: int = 0):
         xr[3, i] = 2.0 * 0.5 * math.cos(th)
     return dict(Ts=Ts, N=N, Ac=Ac, Bc=Bc, Q=Q, R=R, P=P, x_min=x_min, x_max=-x_min,
                 u_min=-8.0, u_max=8.0, xi0=np.array([2.0, 0.0, 0.0, 0.0]), xi_ref=xr)
+
+
+def make_gait_states(p: dict, S: int, seed: int = DEFAULT_SEED, candidates: int = 16):
+    """Per-state data for the on-device input generation (mpcqp_batch_solve_gait), drawn
+    exactly as make_batch draws them: state [S,13], feet [S,6], cmd [S,2] = (0.1 rad/s yaw
+    rate, per-state forward speed), phase [S,C]."""
+    rng = np.random.default_rng(seed)
+    Cc = max(1, candidates)
+    roll = rng.uniform(-0.1, 0.1, S)
+    pitch = rng.uniform(-0.1, 0.1, S)
+    yaw = rng.uniform(-math.pi, math.pi, S)
+    pos = np.stack([rng.uniform(-1, 1, S), rng.uniform(-1, 1, S), rng.uniform(0.76, 0.86, S)], 1)
+    om = rng.normal(0.0, 0.2, (S, 3))
+    vel = np.stack([rng.uniform(-1, 1, S), rng.uniform(-0.3, 0.3, S), rng.normal(0, 0.05, S)], 1)
+    vxr = rng.uniform(0.0, 1.0, S)
+    off_l, off_r = static_foot_offsets()
+    nl = rng.normal(0.0, 0.03, (S, 3))
+    nr = rng.normal(0.0, 0.03, (S, 3))
+    phase = rng.uniform(0.0, 1.0, (S, Cc))
+    state = np.zeros((S, 13))
+    state[:, 0], state[:, 1], state[:, 2] = roll, pitch, yaw
+    state[:, 3:6], state[:, 6:9], state[:, 9:12] = pos, om, vel
+    state[:, 12] = -GRAVITY
+    cy, sy = np.cos(yaw), np.sin(yaw)
+    feet = np.zeros((S, 6))
+    for j, (off, nz) in enumerate(((off_l, nl), (off_r, nr))):
+        o = off[None, :] + nz
+        feet[:, 3 * j] = cy * o[:, 0] - sy * o[:, 1]
+        feet[:, 3 * j + 1] = sy * o[:, 0] + cy * o[:, 1]
+        feet[:, 3 * j + 2] = o[:, 2]
+    cmd = np.stack([np.full(S, 0.1), vxr], 1)
+    return dict(state=state, feet=feet, cmd=cmd, phase=phase)
+
+
+def gait_inputs(p: dict, g: dict):
+    """Host mirror of what mpcqp_batch_solve_gait builds on chip: x0, xref (include/mpcQP.h:
+    74-97), lin = {yaw, r_L, r_R, 0} and contact (MPC::calculateGait) per instance s*C + c."""
+    state, feet, cmd, phase = g["state"], g["feet"], g["cmd"], g["phase"]
+    S, Cc = phase.shape
+    N, Ts = p["N"], p["Ts"]
+    x0 = np.repeat(state, Cc, axis=0)
+    t = np.arange(N + 1) * Ts
+    xr = np.repeat(state[:, None, :], N + 1, axis=1)
+    xr[:, :, 2] = state[:, 2:3] + t[None, :] * cmd[:, 0:1]
+    xr[:, :, 3] = state[:, 3:4] + t[None, :] * cmd[:, 1:2]
+    xr[:, 1:, 9] = cmd[:, 1:2]
+    xr[:, :, 12] = -9.8
+    lin = np.zeros((S, 8))
+    lin[:, 0] = state[:, 2]
+    lin[:, 1:7] = feet
+    contact = np.array([[gait_contact_mask(N, Ts, float(phase[s, c])) for c in range(Cc)]
+                        for s in range(S)], dtype=np.uint64).reshape(-1)
+    return dict(x0=x0, xref=np.repeat(xr, Cc, axis=0), lin=np.repeat(lin, Cc, axis=0),
+                contact=contact)

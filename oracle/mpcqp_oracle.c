@@ -913,3 +913,12 @@ int orc_srbm_batch(const orc_srbm_cfg *cfg, int B, const double *x0, const doubl
     (void)nthreads;
     return ORC_OK;
 }
+
+int orc_srbm_plant(const orc_srbm_cfg *cfg, const double *lin, double *x, const double *u) {
+    double Ac[13 * 13], Bc[13 * 6], Ad[13 * 13], Bd[13 * 6];
+    orc_model_srbm(lin, cfg->mass, cfg->Ib, Ac, Bc);
+    const int rc = orc_discretize(13, 6, cfg->Ts, Ac, Bc, Ad, Bd);
+    if (rc) return rc;
+    orc_plant_step(13, 6, Ad, Bd, x, u);
+    return ORC_OK;
+}

@@ -119,6 +119,10 @@ int orc_srbm_batch(const orc_srbm_cfg *cfg, int B, const double *x0, const doubl
 
 /* per-instance bounds of the SRBM model (contact schedule -> lb/ub) */
 void orc_srbm_bounds(const orc_srbm_cfg *cfg, uint64_t contact, double *lb, double *ub);
+/* SRBM plant step, QPSolver::updateState (src/QPSolver.cpp:108-111) with the exact ZOH of the
+ * SRBM linearised at lin = {yaw, rL, rR}: x <- Ad x + Bd u, (Ad, Bd) = orc_discretize (Eigen's
+ * Pade expm restated).  Returns the discretisation status. */
+int orc_srbm_plant(const orc_srbm_cfg *cfg, const double *lin, double *x, const double *u);
 
 #ifdef __cplusplus
 }

@@ -65,6 +65,7 @@ def lib():
         L.orc_srbm_batch.argtypes = [C.POINTER(SrbmCfg), C.c_int, _dp, _dp, _dp, _up, _dp, _dp,
                                      _ip, _ip, C.c_void_p, C.c_void_p, C.c_int]
         L.orc_srbm_bounds.argtypes = [C.POINTER(SrbmCfg), C.c_uint64, _dp, _dp]
+        L.orc_srbm_plant.argtypes = [C.POINTER(SrbmCfg), _dp, _dp, _dp]
         _lib = L
     return _lib
 
@@ -221,3 +222,14 @@ def srbm_bounds(p, contact):
     lib().orc_srbm_bounds(C.byref(cfg), int(contact), lb, ub)
     del keep
     return lb, ub
+
+
+def srbm_plant(p, lin, x, u):
+    """x+ = Ad x + Bd u of the SRBM at lin (exact ZOH via the Eigen-expm restatement)."""
+    cfg, keep = make_cfg(p)
+    xx = np.ascontiguousarray(x, dtype=np.float64).copy()
+    rc = lib().orc_srbm_plant(C.byref(cfg), np.ascontiguousarray(lin, dtype=np.float64),
+                              xx, np.ascontiguousarray(u, dtype=np.float64))
+    del keep
+    assert rc == 0, rc
+    return xx
