@@ -119,6 +119,27 @@ def host_staged_rate(eng, batch, p, reps=5):
     return B * reps / (time.perf_counter() - t)
 
 
+def gait_fused_rate(eng, p, B, seed, reps=10):
+    """QP/s of mpcqp_batch_solve_gait: the same step with x0/xref/lin/contact generated on
+    chip from per-state data (B/16 states x 16 gait candidates)."""
+    import torch
+
+    import mpcqp
+    if not eng.fast_path or p["model"] != 0:
+        return None
+    Cc = 16
+    g = eng.upload_gait(mpcqp.make_gait_states(p, B // Cc, seed=seed, candidates=Cc))
+    eng.solve_gait(g)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        eng.solve_gait(g)
+    e1.record()
+    torch.cuda.synchronize()
+    return g["B"] * reps / (e0.elapsed_time(e1) * 1e-3)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -225,6 +246,7 @@ def main():
                           whole_step_tflops=dom_flops / (ms_per_step * 1e-3) / 1e12),
         )
         out["config"]["pcie_inclusive_qps"] = host_staged_rate(eng, batch, p)
+        out["config"]["gait_fused_qps"] = gait_fused_rate(eng, p, B, args.seed)
         if not args.no_cpu_baseline:
             cb, _ = cpu_baseline(p, batch)
             out["cpu_baseline"] = cb

@@ -13,6 +13,8 @@
  * ------------------------------  ------------------------------------------------------------
  * mpcqp_discretize                QPSolver::discretizeSystem   src/QPSolver.cpp:21-29
  *                                 (declared include/QPSolver.h:19)
+ * mpcqp_discretize_quadrature     linear_mpc_example discretizeSystem
+ *                                 src/linear_mpc_example.cpp:35-46
  * mpcqp_build_qp                  QPSolver::buildQPParams      src/QPSolver.cpp:31-81
  *                                 (declared include/QPSolver.h:22-25)
  * mpcqp_solve_dense               QPSolver::solveQP            src/QPSolver.cpp:83-106
@@ -74,6 +76,11 @@ extern "C" {
 /* ---- single-instance, reference-compatible entry points (run on the GPU, batch 1) ---- */
 int mpcqp_discretize(int nx, int nu, double Ts, const double *Ac, const double *Bc,
                      double *Ad, double *Bd);
+
+/* linear_mpc_example's discretisation (src/linear_mpc_example.cpp:35-46): Ad = exp(Ac Ts),
+ * Bd = sum_{i<100} Ad (I - Ac tau_i/100)^-1 Bc Ts/100 with tau_i = i Ts/100. */
+int mpcqp_discretize_quadrature(int nx, int nu, double Ts, const double *Ac, const double *Bc,
+                                double *Ad, double *Bd);
 
 /* Outputs use the reference's exact layouts and sizes (nV = nu*N):
  *   H nV x nV, f nV, A_eq (nx*N) x nV, b_eq nx*N, lb/ub nV, A_ineq (2*nx*N) x nV,

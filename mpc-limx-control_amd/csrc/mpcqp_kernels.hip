@@ -196,6 +196,66 @@ __global__ void __launch_bounds__(64) k_plant(int nx, int nu, const double *Ad, 
     }
 }
 
+// linear_mpc_example's numerically integrated Bd (src/linear_mpc_example.cpp:35-46):
+//   Bd = sum_{i<100} Ad (I - Ac tau_i / 100)^-1 Bc Ts/100,  tau_i = i Ts / 100
+// (the reference divides by `steps` twice; kept).  One wave: lane j owns column j of the
+// augmented [W | Bc] for the partial-pivot elimination, then lane (r, c) accumulates
+// (Ad X)(r, c).  Ad comes from the Pade path (k_condense).
+__global__ void __launch_bounds__(64) k_quad_bd(int nx, int nu, double Ts, const double *Ac,
+                                                const double *Bc, const double *Ad, double *Bd) {
+    __shared__ double W[MPCQP_MAX_NX * (MPCQP_MAX_NX + MPCQP_MAX_NU)];
+    __shared__ double acc[MPCQP_MAX_NX * MPCQP_MAX_NU];
+    const int ln = threadIdx.x, nc = nx + nu, steps = 100;
+    for (int e = ln; e < nx * nu; e += 64) acc[e] = 0.0;
+    for (int i = 0; i < steps; ++i) {
+        const double tau = i * Ts / steps;
+        __syncthreads();
+        for (int e = ln; e < nx * nc; e += 64) {  // W column-major nx x nc
+            const int r = e % nx, c = e / nx;
+            double v;
+            if (c < nx) v = -Ac[c * nx + r] * tau / steps + (r == c ? 1.0 : 0.0);
+            else v = Bc[(c - nx) * nx + r];
+            W[e] = v;
+        }
+        __syncthreads();
+        for (int k = 0; k < nx; ++k) {
+            int p = k;
+            double amax = fabs(W[k * nx + k]);
+            for (int r = k + 1; r < nx; ++r) {
+                const double v = fabs(W[k * nx + r]);
+                if (v > amax) { amax = v; p = r; }
+            }
+            const double piv = W[k * nx + p];
+            __syncthreads();
+            if (ln < nc && p != k) {
+                const double t = W[ln * nx + k];
+                W[ln * nx + k] = W[ln * nx + p];
+                W[ln * nx + p] = t;
+            }
+            __syncthreads();
+            if (ln > k && ln < nc)
+                for (int r = k + 1; r < nx; ++r) W[ln * nx + r] -= (W[k * nx + r] / piv) * W[ln * nx + k];
+            __syncthreads();
+        }
+        if (ln >= nx && ln < nc) {  // back substitution of RHS column ln - nx
+            for (int r = nx - 1; r >= 0; --r) {
+                double sum = W[ln * nx + r];
+                for (int l = r + 1; l < nx; ++l) sum -= W[l * nx + r] * W[ln * nx + l];
+                W[ln * nx + r] = sum / W[r * nx + r];
+            }
+        }
+        __syncthreads();
+        for (int e = ln; e < nx * nu; e += 64) {
+            const int r = e % nx, c = e / nx;
+            double sum = 0.0;
+            for (int l = 0; l < nx; ++l) sum += Ad[l * nx + r] * W[(nx + c) * nx + l];
+            acc[e] += sum * (Ts / steps);
+        }
+    }
+    __syncthreads();
+    for (int e = ln; e < nx * nu; e += 64) Bd[e] = acc[e];
+}
+
 // best of each state's C gait candidates: (fp32 cost order bits, candidate) minimum, the same
 // rule as k_select_min; U row copied out.  One wave per state, C <= 64.
 __global__ void __launch_bounds__(64) k_select_state(int S, int C, int nV, const double *cost,
@@ -499,6 +559,24 @@ int mpcqp_discretize(int nx, int nu, double Ts, const double *Ac, const double *
         HIP_TRY(hipMemcpy(Ad, a.ABout, sizeof(double) * nx * nx, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(Bd, a.ABout + nx * nx, sizeof(double) * nx * nu, hipMemcpyDeviceToHost));
     }
+out:
+    return rc;
+}
+
+int mpcqp_discretize_quadrature(int nx, int nu, double Ts, const double *Ac, const double *Bc,
+                                double *Ad, double *Bd) {
+    if (!Ac || !Bc || !Ad || !Bd) return MPCQP_ERR_BAD_ARG;
+    if (nx <= 0 || nu <= 0 || nx > MPCQP_MAX_NX || nu > MPCQP_MAX_NU || nx + nu > 64)
+        return MPCQP_ERR_BAD_DIMS;
+    int rc = mpcqp_discretize(nx, nu, Ts, Ac, Bc, Ad, Bd);  // Ad = exp(Ac Ts) (Pade path)
+    if (rc) return rc;
+    DevBufs bufs;
+    double *dAc = bufs.upload(Ac, (size_t)nx * nx), *dBc = bufs.upload(Bc, (size_t)nx * nu);
+    double *dAd = bufs.upload(Ad, (size_t)nx * nx), *dBd = bufs.alloc<double>((size_t)nx * nu);
+    if (!dAc || !dBc || !dAd || !dBd) return MPCQP_ERR_DEVICE;
+    hipLaunchKernelGGL(k_quad_bd, dim3(1), dim3(64), 0, 0, nx, nu, Ts, dAc, dBc, dAd, dBd);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpy(Bd, dBd, sizeof(double) * nx * nu, hipMemcpyDeviceToHost));
 out:
     return rc;
 }

@@ -21,7 +21,7 @@ CONS_BOX, CONS_FRICTION = 0, 1
 A_ROWMAJOR, A_COLMAJOR = 0, 1
 
 EXPORTS = [
-    "mpcqp_discretize", "mpcqp_build_qp", "mpcqp_solve_dense", "mpcqp_plant_step",
+    "mpcqp_discretize", "mpcqp_discretize_quadrature", "mpcqp_build_qp", "mpcqp_solve_dense", "mpcqp_plant_step",
     "mpcqp_ctx_create", "mpcqp_ctx_destroy", "mpcqp_set_stream", "mpcqp_sync",
     "mpcqp_batch_condense", "mpcqp_batch_solve_qp", "mpcqp_batch_solve",
     "mpcqp_ctx_fast_path", "mpcqp_batch_discretize", "mpcqp_batch_condense_solve",
@@ -64,6 +64,7 @@ def lib():
     vp, dp, ip, i = C.c_void_p, C.c_void_p, C.c_void_p, C.c_int
     d = C.c_double
     L.mpcqp_discretize.argtypes = [i, i, d, vp, vp, vp, vp]
+    L.mpcqp_discretize_quadrature.argtypes = [i, i, d, vp, vp, vp, vp]
     L.mpcqp_build_qp.argtypes = [i, i, i] + [vp] * 7 + [d, d] + [vp] * 11
     L.mpcqp_solve_dense.argtypes = [i, i, vp, vp, vp, i, vp, vp, vp, vp, vp, vp, vp, vp]
     L.mpcqp_plant_step.argtypes = [i, i, vp, vp, vp, vp]

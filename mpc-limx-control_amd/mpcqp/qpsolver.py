@@ -35,15 +35,17 @@ def _p(a):
     return None if a is None else C.c_void_p(a.ctypes.data)
 
 
-def discretize(Ac, Bc, Ts):
+def discretize(Ac, Bc, Ts, quadrature: bool = False):
+    """QPSolver::discretizeSystem (src/QPSolver.cpp:21-29); quadrature=True gives
+    linear_mpc_example's integrated Bd (src/linear_mpc_example.cpp:35-46)."""
     Ac = np.asarray(Ac, float)
     Bc = np.asarray(Bc, float)
     nx, nu = Bc.shape
     Ad = np.zeros(nx * nx)
     Bd = np.zeros(nx * nu)
     fAc, fBc = _f(Ac), _f(Bc)  # keep the buffers alive across the call
-    check("mpcqp_discretize", lib().mpcqp_discretize(nx, nu, float(Ts), _p(fAc), _p(fBc),
-                                                     _p(Ad), _p(Bd)))
+    fn = "mpcqp_discretize_quadrature" if quadrature else "mpcqp_discretize"
+    check(fn, getattr(lib(), fn)(nx, nu, float(Ts), _p(fAc), _p(fBc), _p(Ad), _p(Bd)))
     return Ad.reshape(nx, nx, order="F"), Bd.reshape(nx, nu, order="F")
 
 

@@ -31,6 +31,19 @@ def test_discretize_reference_plant(gpu, golden):
     assert Bd[0, 0] == pytest.approx(2.4991668749583e-4, rel=1e-12)  # SURVEY 8c KAT
 
 
+def test_discretize_quadrature_linear_mpc_example(gpu, golden, orc):
+    """src/linear_mpc_example.cpp:35-46 (the mpc_test harness's Bd) vs the golden fixture"""
+    from mpcqp.qpsolver import discretize
+    g = golden("a0_harness.npz")
+    Ad, Bd = discretize(g["Ac"], g["Bc"], float(g["Ts"]), quadrature=True)
+    assert rel_err(Ad, g["Ad_quad"]) <= TOL_DISC and rel_err(Bd, g["Bd_quad"]) <= TOL_DISC
+    rng = np.random.default_rng(8)
+    Ac, Bc = rng.normal(size=(13, 13)), rng.normal(size=(13, 6))
+    Ad, Bd = discretize(Ac, Bc, 0.01, quadrature=True)
+    Ad0, Bd0 = orc.discretize(Ac, Bc, 0.01, quadrature=True)
+    assert rel_err(Ad, Ad0) <= TOL_DISC and rel_err(Bd, Bd0) <= TOL_DISC
+
+
 @pytest.mark.parametrize("scale", [1e-3, 0.1, 0.5, 1.5, 8.0, 60.0])
 def test_discretize_all_pade_degrees(gpu, orc, scale):
     from mpcqp.qpsolver import discretize
