@@ -39,6 +39,10 @@
  * mpcqp_batch_select_state        (new) best gait candidate per state
  * mpcqp_batch_plant_srbm          QPSolver::updateState (src/QPSolver.cpp:108-111), SRBM, batched
  * mpcqp_rollout                   the closed loop of src/qpSolver_test.cpp:38-90, batched
+ * mpcqp_fk_feet                   PinocchioKinematics::forwardKinematics + getLinkPosition
+ *                                 (include/pinocchio_kinematics.h:30-43), batched
+ * mpcqp_kf_update                 stateEstimator::update (include/stateEstimator.h:217-337),
+ *                                 batched
  */
 #ifndef MPCQP_H
 #define MPCQP_H
@@ -205,6 +209,23 @@ int mpcqp_batch_plant_srbm(mpcqp_ctx *ctx, int S, int C, double *state, double *
 int mpcqp_rollout(mpcqp_ctx *ctx, int S, int C, int K, double *state, double *feet,
                   const double *cmd, double *phase, float swing, float stance, double *traj,
                   int *choice);
+
+/* ---- producers either side of the step, device pointers, async on
+ * `stream` (a hipStream_t; NULL = the null stream) ----------------------------------------
+ * Foot contact points of both 3-DoF legs, world frame relative to the base -> the `feet` of
+ * mpcqp_batch_solve_gait.  q [R][6] = (abad, hip, knee) left then right; rpy with row stride
+ * rpy_stride (3 for [R][3], 13 to read a state [R][13]).  Replaces Pinocchio FK
+ * (include/pinocchio_kinematics.h:30-43); chain from MPCParam's kinematicValues
+ * (include/MPCParam.h:13-38), at q = 0 equal to static_foot_offset_* (:64-72). */
+int mpcqp_fk_feet(void *stream, int R, const double *q, const double *rpy, int rpy_stride,
+                  double *feet);
+/* One step of stateEstimator::update (include/stateEstimator.h:217-337) for R robots:
+ * xhat [R][12] (p, v, foot positions), P [R][144] (column-major) updated in place from
+ * eePos/eeVel [R][6] (feet relative to the base), contact [R][2], quat [R][4] (x y z w),
+ * acc [R][3] (IMU, body frame). */
+int mpcqp_kf_update(void *stream, int R, double dt, double *xhat, double *P, const double *eePos,
+                    const double *eeVel, const unsigned char *contact, const double *quat,
+                    const double *acc);
 
 /* duration of the last stage-1 (which = 0: discretize / generic condense) or stage-2
  * (which = 1: condense_solve / generic solve) kernel, HIP events on the ctx stream (ms; -1 if

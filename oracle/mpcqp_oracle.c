@@ -922,3 +922,171 @@ int orc_srbm_plant(const orc_srbm_cfg *cfg, const double *lin, double *x, const 
     orc_plant_step(13, 6, Ad, Bd, x, u);
     return ORC_OK;
 }
+
+/* ---- state estimator: stateEstimator::update, include/stateEstimator.h:217-337
+ * One linear Kalman step of the 12-state estimator [p(3), v(3), foot positions(6)] with 14
+ * measurements [-eePos (+foot radius on z), -eeVel, feetHeights(2) = 0].  Restated as
+ * written, quirks included: dt*9.81f/20.f (float literal), q_(6:12) = dt I, the `y << ps, vs,
+ * feetHeights_` of a 4-vector keeping its first two (zero) entries, accel = R(zyx)' a + g,
+ * the symmetrisation and the det(P(0:2,0:2)) > 1e-6 decoupling.  R(zyx) is ocs2's
+ * getRotationMatrixFromZyxEulerAngles (Rz Ry Rx; ocs2 is not vendored, restated). */
+static void quat_to_zyx(const double *q /* x y z w */, double *zyx) {
+    const double x = q[0], y = q[1], z = q[2], w = q[3];
+    double as = -2. * (x * z - w * y);
+    if (as > .99999) as = .99999;
+    zyx[0] = atan2(2 * (x * y + w * z), w * w + x * x - y * y - z * z);
+    zyx[1] = asin(as);
+    zyx[2] = atan2(2 * (y * z + w * x), w * w - x * x - y * y + z * z);
+}
+static void rot_zyx(const double *e, double *R /* col-major */) {
+    const double c1 = cos(e[0]), c2 = cos(e[1]), c3 = cos(e[2]);
+    const double s1 = sin(e[0]), s2 = sin(e[1]), s3 = sin(e[2]);
+    R[IDX(0, 0, 3)] = c1 * c2; R[IDX(0, 1, 3)] = c1 * s2 * s3 - s1 * c3; R[IDX(0, 2, 3)] = c1 * s2 * c3 + s1 * s3;
+    R[IDX(1, 0, 3)] = c2 * s1; R[IDX(1, 1, 3)] = s1 * s2 * s3 + c1 * c3; R[IDX(1, 2, 3)] = s1 * s2 * c3 - c1 * s3;
+    R[IDX(2, 0, 3)] = -s2;     R[IDX(2, 1, 3)] = c2 * s3;                R[IDX(2, 2, 3)] = c2 * c3;
+}
+
+int orc_kf_update(double dt, double *xhat, double *P, const double *eePos, const double *eeVel,
+                  const unsigned char *contact, const double *quat, const double *acc) {
+    double A[144] = {0}, B[36] = {0}, Cm[168] = {0}, qd[12], rd[14], y[14];
+    for (int i = 0; i < 12; ++i) A[IDX(i, i, 12)] = 1.0;
+    for (int i = 0; i < 3; ++i) {
+        A[IDX(i, 3 + i, 12)] = dt;
+        B[IDX(i, i, 12)] = 0.5 * dt * dt;
+        B[IDX(3 + i, i, 12)] = dt;
+    }
+    for (int i = 0; i < 3; ++i) {
+        Cm[IDX(i, i, 14)] = 1.0; Cm[IDX(3 + i, i, 14)] = 1.0;          /* c1 blocks */
+        Cm[IDX(6 + i, 3 + i, 14)] = 1.0; Cm[IDX(9 + i, 3 + i, 14)] = 1.0; /* c2 blocks */
+    }
+    for (int i = 0; i < 6; ++i) Cm[IDX(i, 6 + i, 14)] = -1.0;
+    Cm[IDX(12, 8, 14)] = 1.0;
+    Cm[IDX(13, 11, 14)] = 1.0;
+    for (int i = 0; i < 3; ++i) {
+        qd[i] = (dt / 20.f) * 0.02;
+        qd[3 + i] = (dt * 9.81f / 20.f) * 0.02;
+    }
+    for (int i = 6; i < 12; ++i) qd[i] = dt * 0.002;
+    for (int i = 0; i < 6; ++i) rd[i] = 0.005;
+    for (int i = 6; i < 12; ++i) rd[i] = 0.1;
+    rd[12] = rd[13] = 0.01;
+    for (int f = 0; f < 2; ++f) {
+        const double k = contact[f] ? 1.0 : 100.0;
+        for (int d = 0; d < 3; ++d) {
+            qd[6 + 3 * f + d] *= k;
+            rd[3 * f + d] *= k;
+            rd[6 + 3 * f + d] *= k;
+            y[3 * f + d] = -eePos[3 * f + d] + (d == 2 ? 0.02 : 0.0);
+            y[6 + 3 * f + d] = -eeVel[3 * f + d];
+        }
+        rd[12 + f] *= k;
+    }
+    y[12] = y[13] = 0.0;
+    double zyx[3], R[9], accw[3];
+    quat_to_zyx(quat, zyx);
+    rot_zyx(zyx, R);
+    for (int i = 0; i < 3; ++i) {
+        double s = 0.0;
+        for (int l = 0; l < 3; ++l) s += R[IDX(l, i, 3)] * acc[l]; /* R' a */
+        accw[i] = s + (i == 2 ? -9.81 : 0.0);
+    }
+    double xn[12], T[144], Pm[144];
+    for (int i = 0; i < 12; ++i) {
+        double s = 0.0;
+        for (int l = 0; l < 12; ++l) s += A[IDX(i, l, 12)] * xhat[l];
+        for (int l = 0; l < 3; ++l) s += B[IDX(i, l, 12)] * accw[l];
+        xn[i] = s;
+    }
+    mm(12, 12, 12, A, P, T);
+    for (int j = 0; j < 12; ++j)
+        for (int i = 0; i < 12; ++i) {
+            double s = 0.0;
+            for (int l = 0; l < 12; ++l) s += T[IDX(i, l, 12)] * A[IDX(j, l, 12)];
+            Pm[IDX(i, j, 12)] = s + (i == j ? qd[i] : 0.0);
+        }
+    double PC[168], S[196], ey[14], X[14 * 13];
+    for (int j = 0; j < 14; ++j) /* PC = Pm C' (12 x 14) */
+        for (int i = 0; i < 12; ++i) {
+            double s = 0.0;
+            for (int l = 0; l < 12; ++l) s += Pm[IDX(i, l, 12)] * Cm[IDX(j, l, 14)];
+            PC[IDX(i, j, 12)] = s;
+        }
+    for (int j = 0; j < 14; ++j)
+        for (int i = 0; i < 14; ++i) {
+            double s = 0.0;
+            for (int l = 0; l < 12; ++l) s += Cm[IDX(i, l, 14)] * PC[IDX(l, j, 12)];
+            S[IDX(i, j, 14)] = s + (i == j ? rd[i] : 0.0);
+        }
+    for (int i = 0; i < 14; ++i) {
+        double s = 0.0;
+        for (int l = 0; l < 12; ++l) s += Cm[IDX(i, l, 14)] * xn[l];
+        ey[i] = y[i] - s;
+    }
+    for (int i = 0; i < 14; ++i) X[IDX(i, 0, 14)] = ey[i];
+    for (int j = 0; j < 12; ++j)
+        for (int i = 0; i < 14; ++i) X[IDX(i, 1 + j, 14)] = Cm[IDX(i, j, 14)];
+    if (lu_solve(14, S, 13, X)) return ORC_NOT_PD;
+    for (int i = 0; i < 12; ++i) {
+        double s = 0.0;
+        for (int l = 0; l < 14; ++l) s += PC[IDX(i, l, 12)] * X[IDX(l, 0, 14)];
+        xhat[i] = xn[i] + s;
+    }
+    double K[144], Pn[144]; /* K = I - PC sC */
+    for (int j = 0; j < 12; ++j)
+        for (int i = 0; i < 12; ++i) {
+            double s = 0.0;
+            for (int l = 0; l < 14; ++l) s += PC[IDX(i, l, 12)] * X[IDX(l, 1 + j, 14)];
+            K[IDX(i, j, 12)] = (i == j ? 1.0 : 0.0) - s;
+        }
+    mm(12, 12, 12, K, Pm, Pn);
+    for (int j = 0; j < 12; ++j)
+        for (int i = 0; i < 12; ++i) P[IDX(i, j, 12)] = (Pn[IDX(i, j, 12)] + Pn[IDX(j, i, 12)]) / 2.0;
+    const double det = P[IDX(0, 0, 12)] * P[IDX(1, 1, 12)] - P[IDX(0, 1, 12)] * P[IDX(1, 0, 12)];
+    if (det > 0.000001) {
+        for (int j = 2; j < 12; ++j)
+            for (int i = 0; i < 2; ++i) { P[IDX(i, j, 12)] = 0.0; P[IDX(j, i, 12)] = 0.0; }
+        for (int j = 0; j < 2; ++j)
+            for (int i = 0; i < 2; ++i) P[IDX(i, j, 12)] /= 10.;
+    }
+    return ORC_OK;
+}
+
+/* ---- leg kinematics: foot contact points of the two 3-DoF legs.
+ * The reference computes them with Pinocchio from PF_TRON1A's URDF
+ * (include/pinocchio_kinematics.h:30-43), which is not in the repository; the chain is
+ * restated from MPCParam's kinematicValues (include/MPCParam.h:13-38) with the usual
+ * point-foot axes (abad about x, hip and knee about y -- build-chosen), and the left leg's
+ * lateral sign convention of MPCParam.h:66-72.  At q = 0 it reproduces the reference's
+ * static_foot_offset_{left,right} exactly (the pinned known answer).
+ *   p_body = abad + Rx(q0) (hip + Ry(q1) (knee + Ry(q2) (foot + contact)))
+ *   feet   = R(rpy) p_body, R = Rz(yaw) Ry(pitch) Rx(roll)  (world frame, foot minus base) */
+static const double K_ABAD[3] = {0.05556, 0.105, -0.2602}, K_HIP[3] = {-0.077, 0.02050, 0.0},
+                    K_KNEE[3] = {-0.1500, -0.02050, -0.25981}, K_FOOT[3] = {0.145, 0.0, -0.2598},
+                    K_CONTACT[3] = {0.0, 0.0, -0.032};
+
+void orc_fk_feet(const double *q, const double *rpy, double *feet) {
+    const double cr = cos(rpy[0]), sr = sin(rpy[0]), cp = cos(rpy[1]), sp = sin(rpy[1]),
+                 cyw = cos(rpy[2]), syw = sin(rpy[2]);
+    for (int leg = 0; leg < 2; ++leg) {
+        const double sg = leg == 0 ? -1.0 : 1.0;
+        const double *ql = q + 3 * leg;
+        double v[3] = {K_FOOT[0] + K_CONTACT[0], K_FOOT[1] + K_CONTACT[1], K_FOOT[2] + K_CONTACT[2]};
+        /* knee: Ry(q2) v + knee */
+        double c = cos(ql[2]), s = sin(ql[2]), t0 = c * v[0] + s * v[2], t2 = -s * v[0] + c * v[2];
+        v[0] = t0 + K_KNEE[0]; v[1] = v[1] + sg * K_KNEE[1]; v[2] = t2 + K_KNEE[2];
+        /* hip: Ry(q1) v + hip */
+        c = cos(ql[1]); s = sin(ql[1]); t0 = c * v[0] + s * v[2]; t2 = -s * v[0] + c * v[2];
+        v[0] = t0 + K_HIP[0]; v[1] = v[1] + sg * K_HIP[1]; v[2] = t2 + K_HIP[2];
+        /* abad: Rx(q0) v + abad */
+        c = cos(ql[0]); s = sin(ql[0]);
+        const double t1 = c * v[1] - s * v[2];
+        t2 = s * v[1] + c * v[2];
+        v[0] = v[0] + K_ABAD[0]; v[1] = t1 + sg * K_ABAD[1]; v[2] = t2 + K_ABAD[2];
+        /* world: Rz Ry Rx v */
+        const double a1 = v[1] * cr - v[2] * sr, a2 = v[1] * sr + v[2] * cr;   /* Rx */
+        const double b0 = v[0] * cp + a2 * sp, b2 = -v[0] * sp + a2 * cp;      /* Ry */
+        feet[3 * leg + 0] = b0 * cyw - a1 * syw;                               /* Rz */
+        feet[3 * leg + 1] = b0 * syw + a1 * cyw;
+        feet[3 * leg + 2] = b2;
+    }
+}

@@ -124,6 +124,16 @@ void orc_srbm_bounds(const orc_srbm_cfg *cfg, uint64_t contact, double *lb, doub
  * Pade expm restated).  Returns the discretisation status. */
 int orc_srbm_plant(const orc_srbm_cfg *cfg, const double *lin, double *x, const double *u);
 
+/* ---- state estimator and leg kinematics ------------------------ */
+/* stateEstimator::update (include/stateEstimator.h:217-337), one robot: xhat[12], P[144]
+ * (col-major) updated in place from eePos[6], eeVel[6] (feet relative to the base, world
+ * frame, as eeKinematics_ returns them), contact[2], quat[4] (x y z w), acc[3] (IMU, local) */
+int orc_kf_update(double dt, double *xhat, double *P, const double *eePos, const double *eeVel,
+                  const unsigned char *contact, const double *quat, const double *acc);
+/* foot contact points of both legs, world frame relative to the base: q[6] = (abad, hip, knee)
+ * left then right, rpy[3]; feet[6] = left xyz, right xyz (chain in mpcqp_oracle.c) */
+void orc_fk_feet(const double *q, const double *rpy, double *feet);
+
 #ifdef __cplusplus
 }
 #endif

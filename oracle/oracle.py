@@ -66,6 +66,8 @@ def lib():
                                      _ip, _ip, C.c_void_p, C.c_void_p, C.c_int]
         L.orc_srbm_bounds.argtypes = [C.POINTER(SrbmCfg), C.c_uint64, _dp, _dp]
         L.orc_srbm_plant.argtypes = [C.POINTER(SrbmCfg), _dp, _dp, _dp]
+        L.orc_fk_feet.argtypes = [_dp, _dp, _dp]
+        L.orc_kf_update.argtypes = [C.c_double, _dp, _dp, _dp, _dp, C.c_void_p, _dp, _dp]
         _lib = L
     return _lib
 
@@ -233,3 +235,23 @@ def srbm_plant(p, lin, x, u):
     del keep
     assert rc == 0, rc
     return xx
+
+
+def kf_update(dt, xhat, P, eePos, eeVel, contact, quat, acc):
+    """stateEstimator::update restated (one robot) -> (xhat, P)"""
+    x = np.ascontiguousarray(xhat, dtype=np.float64).copy()
+    Pm = np.asfortranarray(np.asarray(P, dtype=np.float64)).reshape(-1, order="F").copy()
+    ct = np.ascontiguousarray(contact, dtype=np.uint8)
+    rc = lib().orc_kf_update(float(dt), x, Pm, np.ascontiguousarray(eePos, dtype=np.float64),
+                             np.ascontiguousarray(eeVel, dtype=np.float64),
+                             C.c_void_p(ct.ctypes.data), np.ascontiguousarray(quat, dtype=np.float64),
+                             np.ascontiguousarray(acc, dtype=np.float64))
+    assert rc == 0, rc
+    return x, Pm.reshape(12, 12, order="F")
+
+
+def fk_feet(q, rpy):
+    out = np.zeros(6)
+    lib().orc_fk_feet(np.ascontiguousarray(q, dtype=np.float64),
+                      np.ascontiguousarray(rpy, dtype=np.float64), out)
+    return out
