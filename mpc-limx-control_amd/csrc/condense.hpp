@@ -46,16 +46,21 @@ __device__ __forceinline__ double srbm_entry(int i, int j, const double *lin, do
     if (i >= 6 && i < 9) {  // Iw^-1 [r_ft]x, column c
         // selects instead of indexing, so a lane-varying i or j never forces the small
         // arrays into scratch
-        const double r0 = ft ? lin[4] : lin[1], r1 = ft ? lin[5] : lin[2], r2 = ft ? lin[6] : lin[3];
+        const double f1 = ft ? 1.0 : 0.0, f0 = 1.0 - f1;
+        const double r0 = f0 * lin[1] + f1 * lin[4], r1 = f0 * lin[2] + f1 * lin[5],
+                     r2 = f0 * lin[3] + f1 * lin[6];
         // column c of [r]x
         double x0, x1, x2;
         if (c == 0) { x0 = 0.0; x1 = r2; x2 = -r1; }
         else if (c == 1) { x0 = -r2; x1 = 0.0; x2 = r0; }
         else { x0 = r1; x1 = -r0; x2 = 0.0; }
+        // row ii of Iw^-1 by arithmetic blending: a select of two array loads would be folded
+        // into one load with a lane-varying index, which keeps the array in scratch memory
         const int ii = i - 6;
-        const double w0 = ii == 0 ? Iwi[0] : (ii == 1 ? Iwi[1] : Iwi[2]);
-        const double w1 = ii == 0 ? Iwi[3] : (ii == 1 ? Iwi[4] : Iwi[5]);
-        const double w2 = ii == 0 ? Iwi[6] : (ii == 1 ? Iwi[7] : Iwi[8]);
+        const double e0 = ii == 0 ? 1.0 : 0.0, e1 = ii == 1 ? 1.0 : 0.0, e2 = ii == 2 ? 1.0 : 0.0;
+        const double w0 = e0 * Iwi[0] + e1 * Iwi[1] + e2 * Iwi[2];
+        const double w1 = e0 * Iwi[3] + e1 * Iwi[4] + e2 * Iwi[5];
+        const double w2 = e0 * Iwi[6] + e1 * Iwi[7] + e2 * Iwi[8];
         return w0 * x0 + w1 * x1 + w2 * x2;
     }
     if (i >= 9 && i < 12) return (i - 9 == c) ? 1.0 / mass : 0.0;

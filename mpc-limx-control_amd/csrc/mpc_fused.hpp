@@ -72,6 +72,18 @@ __device__ __forceinline__ uint64_t gait_mask_wave(int N, double Ts, double phas
     return spread_even(left) | (spread_even(right) << 1);
 }
 
+// Nonzero rows of X0 = Bc Ts and X1 = Ac Bc Ts^2 for the two TRON1 models (compile time):
+// SRBM: Bc rows 6-11 (omega, v), Ac maps those to rows 0-5 (Theta, p); literal: Bc rows 9-11,
+// Ac maps them to rows 3-5.  The supports are disjoint, so X0' W X1 = 0 for diagonal W: only
+// the (0,0) and (1,1) blocks of S^W are nonzero, each over the support rows only.
+template <int MODEL>
+struct XSupport {
+    static constexpr int x0lo = MODEL == 0 ? 6 : 9, x0hi = 12;
+    static constexpr int x1lo = MODEL == 0 ? 0 : 3, x1hi = 6;
+    static_assert(x0hi - x0lo == x1hi - x1lo, "equal support sizes");
+    static_assert(x1hi <= x0lo, "disjoint supports");
+};
+
 template <int NU, int N, bool FRIC, int NF>
 struct MpcLayout {
     static constexpr int NX = 13, NV = NU * N, LD = NF | 1;
@@ -256,33 +268,38 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     MPCQP_STAMP(a.stamps, 0, tst);
     MPCQP_CUT(a.cut, 1);
 
-    // ---- S^W_rs = X_r' W X_s   (w: 0 = Q, 1 = P), stored [w][r][s][cj][ci]; the block
-    //      loop is wave-uniform so the weights are scalar loads
+    // ---- S^W_rr = X_r' W X_r over the support rows (w: 0 = Q, 1 = P); slot rs = 4w + 3r of
+    //      entry o = cj NU + ci (the cross blocks rs = 1, 2, 5, 6 are zero and never read).
+    //      The block loop is wave-uniform so the weights are scalar loads.
+    using Sup = XSupport<MODEL>;
+    constexpr int SD = Sup::x0hi - Sup::x0lo;
 #pragma unroll
-    for (int rs = 0; rs < 8; ++rs) {
-        const int s_ = rs & 1, r_ = (rs >> 1) & 1, w_ = rs >> 2;
-        const double *Xr = r_ ? X1 : X0, *Xs = s_ ? X1 : X0;
+    for (int blk = 0; blk < 4; ++blk) {
+        const int r_ = blk & 1, w_ = blk >> 1, rs = 4 * w_ + 3 * r_;
+        const int lo = r_ ? Sup::x1lo : Sup::x0lo;
+        const double *Xr = r_ ? X1 : X0;
         const double *w = w_ ? a.pd : a.qd;
         for (int e = ln; e < NU * NU; e += kWave) {
             const int ci = e % NU, cj = e / NU;
             double acc = 0.0;
 #pragma unroll
-            for (int l = 0; l < NX; ++l) acc += Xr[ci * NX + l] * w[l] * Xs[cj * NX + l];
-            S[e * 8 + rs] = acc;  // [o = cj NU + ci][rs]: one entry's 8 terms contiguous
+            for (int l = lo; l < lo + SD; ++l) acc += Xr[ci * NX + l] * w[l] * Xr[cj * NX + l];
+            S[e * 8 + rs] = acc;  // [o = cj NU + ci][rs]: one entry's terms contiguous
         }
     }
-    // ---- u_m(c) = X0[:,c]' W_m e_m, v_m(c) = X1[:,c]' W_m e_m, m = 1..N
+    // ---- u_m(c) = X0[:,c]' W_m e_m, v_m(c) = X1[:,c]' W_m e_m, m = 1..N (support rows only)
     for (int e = ln; e < N * NU; e += kWave) {
         const int c = e % NU, m = 1 + e / NU;
         const double md = (double)m, hm2 = 0.5 * md * md;
+        auto el = [&](int l) {
+            const double wl = (m < N) ? a.qd[l] : a.pd[l];
+            return wl * (x0g[l] + md * Ax[l] + hm2 * A2x[l] - xr[m * NX + l]);
+        };
         double su = 0.0, sv = 0.0;
 #pragma unroll
-        for (int l = 0; l < NX; ++l) {
-            const double wl = (m < N) ? a.qd[l] : a.pd[l];
-            const double el = wl * (x0g[l] + md * Ax[l] + hm2 * A2x[l] - xr[m * NX + l]);
-            su += X0[c * NX + l] * el;
-            sv += X1[c * NX + l] * el;
-        }
+        for (int l = Sup::x0lo; l < Sup::x0hi; ++l) su += X0[c * NX + l] * el(l);
+#pragma unroll
+        for (int l = Sup::x1lo; l < Sup::x1hi; ++l) sv += X1[c * NX + l] * el(l);
         UV[(m * 2 + 0) * NU + c] = su;
         UV[(m * 2 + 1) * NU + c] = sv;
     }
@@ -299,9 +316,10 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
         double c, si, sj, sij;
         beta_sums(kk + 1, N - 1, ki, kj, c, si, sj, sij);
         const double bi = (double)(N - 1 - ki) + 0.5, bj = (double)(N - 1 - kj) + 0.5;
-        const double *So = S + (cj * NU + ci) * 8;
-        double v = c * So[0] + sj * So[1] + si * So[2] + sij * So[3];
-        v += So[4] + bj * So[5] + bi * So[6] + bi * bj * So[7];
+        const double *So = S + (cj * NU + ci) * 8;  // cross blocks are zero (XSupport)
+        (void)si; (void)sj;
+        double v = c * So[0] + sij * So[3];
+        v += So[4] + bi * bj * So[7];
         if (ki == kj) v += D[Lay::oRm + cj * NU + ci];
         return 2.0 * v;
     };
@@ -345,8 +363,8 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
                         const int cj = __builtin_ctz(rj), qq = pos[kj * NU + cj];
                         if (pp >= qq) {
                             const double *So = S + (cj * NU + ci) * 8;
-                            double v = c * So[0] + sj * So[1] + si * So[2] + sij * So[3];
-                            v += So[4] + bj * So[5] + bi * So[6] + bij * So[7];
+                            double v = c * So[0] + sij * So[3];  // cross blocks zero
+                            v += So[4] + bij * So[7];
                             if (ki == kj) v += D[Lay::oRm + cj * NU + ci];
                             Hb[lrow(pp) + qq] = 2.0 * v;
                         }
