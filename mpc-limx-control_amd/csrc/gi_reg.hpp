@@ -100,8 +100,9 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
     double fval = 0.0, x = 0.0, u = 0.0;
     int iters = 0, q = 0, act = -1;
     double Jr[NF];
-    double gv = g;     // lane i: g_i, then t_i = (L^-1 g)_i
-    double dinv = 1.0; // lane i: 1 / L(i,i)
+    constexpr bool T63 = NF < kWave;  // lane 63 computes t = L^-1 g in the inverse sweep
+    double gv = g;     // lane i: g_i, then t_i = (L^-1 g)_i (fused path, NF == 64)
+    double dinv = 1.0; // lane i: 1 / L(i,i) (fused path)
     double *colb = rowbuf + NF, *rot = rowbuf + 2 * NF;
     MPCQP_STAMP_INIT(tst);
 
@@ -111,17 +112,21 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         //      is never read).  The forward solve L t = g runs in the same sweep.
         //      Look-ahead: lane k+1's own L(k+1,k) gives the next pivot without waiting for
         //      the LDS broadcast, so the pivot's rsqrt overlaps the step's bulk update.
+        //      With NF < 64, lane 63 is free: it carries g as an extra column through the
+        //      inverse sweep instead (T63), which keeps the forward solve out of this loop.
         double piv = readlane(h[0], 0);
         bool bad = !(piv > 0.0);
         double ik = rsqrt_nr(piv);
 #pragma unroll
         for (int k = 0; k < NF; ++k) {
-            const double lkk = piv * ik;
-            const double lik = (ln == k) ? lkk : h[k] * ik;
-            const double tk = readlane(gv, k) * ik;
+            // on lane k, h[k] is the pivot itself, so lik there is L(k,k) = piv / sqrt(piv)
+            const double lik = h[k] * ik;
             h[k] = lik;
-            gv = (ln == k) ? tk : ((ln > k) ? gv - lik * tk : gv);
-            dinv = (ln == k) ? ik : dinv;
+            if constexpr (!T63) {
+                const double tk = readlane(gv, k) * ik;
+                gv = (ln == k) ? tk : ((ln > k) ? gv - lik * tk : gv);
+                dinv = (ln == k) ? ik : dinv;
+            }
             if (ln > k && ln < NF) colb[ln] = lik;  // column k of L, broadcast through LDS
             double pivn = 1.0, ikn = 1.0;
             if (k + 1 < NF) {
@@ -139,8 +144,10 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
 #pragma unroll
             for (int j = 0; j < NF; ++j)
                 if (j >= k) pin(h[j]);  // step k's updates happen in step k
-            pin(gv);
-            pin(dinv);
+            if constexpr (!T63) {
+                pin(gv);
+                pin(dinv);
+            }
             piv = pivn;
             ik = ikn;
             pin(piv);
@@ -157,7 +164,12 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
 #pragma unroll
             for (int l = 0; l < NF; ++l)
                 if (l <= ln) Lp[lrow(ln) + l] = h[l];
-            rowbuf[ln] = dinv;
+            if constexpr (!T63) rowbuf[ln] = dinv;
+        }
+        if constexpr (T63) {
+            if (ln < NF) colb[ln] = gv;  // g, read by lane 63 as its right-hand side
+            wave_sync();
+            if (ln < NF) rowbuf[ln] = 1.0 / Lp[lrow(ln) + ln];
         }
         wave_sync();
         // ---- columns of L^-1 (lane c); L(i,l) are uniform-address LDS broadcasts, so only
@@ -166,6 +178,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         for (int i = 0; i < NF; ++i) {
             // four partial sums: the dot product is an FMA-latency chain otherwise
             double s4[4] = {(ln == i) ? 1.0 : 0.0, 0.0, 0.0, 0.0};
+            if constexpr (T63) s4[0] = (ln == kWave - 1) ? colb[i] : s4[0];
 #pragma unroll
             for (int l = 0; l < NF; ++l) {
                 if (l < i) s4[l & 3] -= Lp[lrow(i) + l] * Jr[l];
@@ -177,8 +190,17 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         }
         MPCQP_STAMP(C.stamps, 6, tst); MPCQP_CUT(C.cut, 5);
         // ---- unconstrained minimum x = -J t, objective -|t|^2/2 (t_j = 0 beyond nf)
-        if (ln < NF) colb[ln] = gv;
+        if constexpr (T63) {
+            wave_sync();
+            if (ln == kWave - 1) {  // lane 63 publishes t (its Jr row); its Jr is junk from now
+#pragma unroll
+                for (int j = 0; j < NF; ++j) colb[j] = Jr[j];
+            }
+        } else {
+            if (ln < NF) colb[ln] = gv;
+        }
         wave_sync();
+        if constexpr (T63) gv = (ln < NF) ? colb[ln] : 0.0;
         double s4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int j = 0; j < NF; ++j) {
