@@ -86,33 +86,42 @@ struct XSupport {
 
 template <int NU, int N, bool FRIC, int NF>
 struct MpcLayout {
+    static_assert(NF <= 64, "the register solver holds at most 64 free variables");
     static constexpr int NX = 13, NV = NU * N, LD = NF | 1;
     static constexpr int NFRIC = FRIC ? 4 * N * 2 : 0;
     static constexpr int MT = 2 * NF + NFRIC;
-    static constexpr bool REG = NF <= 64;
-    static constexpr int NR0 = REG ? RegPack<NF>::doubles : NF * LD;
-    static constexpr int NR = NR0 > NX * (NX + NU) ? NR0 : NX * (NX + NU);  // also model scratch
-    // doubles
-    static constexpr int oX0 = 0;                        // B  (NX x NU)
-    static constexpr int oX1 = oX0 + NX * NU;            // AB (NX x NU)
-    static constexpr int oS = oX1 + NX * NU;             // S[w][r][s] (8 x NU x NU)
-    static constexpr int oUV = oS + 8 * NU * NU;         // u_m, v_m: [(N+1)][2][NU]
-    static constexpr int oAx = oUV + (N + 1) * 2 * NU;   // A x0 (NX), A^2 x0 (NX)
-    static constexpr int oR = oAx + 2 * NX;              // R factor (packed / NF x LD)
-    static constexpr int oJ = oR + NR;                   // J (LDS solver only)
-    static constexpr int oRow = oJ + (REG ? 0 : NF * LD);// broadcast buffers (4 NF)
-    static constexpr int oG = oRow + 4 * NF;             // g (LDS solver)
-    static constexpr int oXS = oG + NF;
-    static constexpr int oXF = oXS + NF;                 // xfull (NV)
-    static constexpr int oMisc = oXF + NV;               // rowfix / ys slot
-    static constexpr int oXr = oMisc + 2;                // xref (NX x (N+1)) prefetch
-    static constexpr int oX0v = oXr + NX * (N + 1);      // x0 prefetch (NX)
-    static constexpr int oRm = oX0v + NX + 1;            // R (NU x NU) copy
-    static constexpr int nDoubles = oRm + NU * NU;
+    static constexpr bool REG = true;
+    static constexpr int NR = RegPack<NF>::doubles;  // packed L / R
+    // doubles.  Live for the whole kernel: S (4 nonzero blocks, entry-major), u/v, R copy,
+    // x mirror, fixed values; then one region the phases take turns on:
+    //   model/condensing: T = [Ac | Bc] (scratch), X0, X1, A x0, A^2 x0, xref, x0
+    //   H_FF build      : packed H (first nf(nf+1)/2 doubles)
+    //   solver          : packed L / R, then the 4 NF broadcast buffers
+    static constexpr int oS = 0;                          // [NU*NU][4]
+    static constexpr int oUV = oS + 4 * NU * NU;          // u_m, v_m: [(N+1)][2][NU]
+    static constexpr int oRm = oUV + (N + 1) * 2 * NU;    // R (NU x NU) copy
+    static constexpr int oXS = oRm + NU * NU;             // x mirror (NF)
+    static constexpr int oXF = oXS + NF;                  // xfull (NV)
+    static constexpr int oMisc = oXF + NV;                // rowfix / ys slot
+    static constexpr int oU = (oMisc + 2 + 1) & ~1;       // the shared region (16-B aligned)
+    // early-phase view of the shared region
+    static constexpr int oT = oU;                         // [Ac | Bc] (NX x (NX+NU))
+    static constexpr int oX0 = oT + NX * (NX + NU);       // B  (NX x NU)
+    static constexpr int oX1 = oX0 + NX * NU;             // AB (NX x NU)
+    static constexpr int oAx = oX1 + NX * NU;             // A x0, A^2 x0 (2 NX)
+    static constexpr int oXr = oAx + 2 * NX;              // xref (NX x (N+1))
+    static constexpr int oX0v = oXr + NX * (N + 1);       // x0 (NX)
+    static constexpr int nEarly = oX0v + NX + 1 - oU;
+    // solver view
+    static constexpr int oR = oU;                         // packed L / R (and H_FF before)
+    static constexpr int oRow = (oR + NR + 1) & ~1;       // broadcast buffers (4 NF)
+    static constexpr int nLate = oRow + 4 * NF - oU;
+    static constexpr int nDoubles = oU + (nEarly > nLate ? nEarly : nLate);
     static constexpr size_t bytes =
         sizeof(double) * nDoubles + sizeof(int) * (NF + NV) + ((MT + 15) & ~15);
     static constexpr size_t lds_bytes = (bytes + 15) & ~(size_t)15;
-    static_assert(oRow % 2 == 0, "broadcast buffers must be 16-byte aligned");
+    static_assert(oRow % 2 == 0 && oU % 2 == 0, "16-byte aligned buffers");
+    static_assert(NF * (NF + 1) / 2 <= NR, "packed H fits the L / R space");
 };
 
 // sum over m in [m0, m1] of 1, beta_i, beta_j, beta_i beta_j; beta_x = m - 1 - k_x + 1/2
@@ -138,6 +147,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     const int b = blockIdx.x, ln = lane();
     double *D = reinterpret_cast<double *>(smem);
     double *X0 = D + Lay::oX0, *X1 = D + Lay::oX1, *S = D + Lay::oS, *UV = D + Lay::oUV;
+    static_assert(MODEL == 0 || MODEL == 1, "TRON1 models only");
     double *Ax = D + Lay::oAx, *A2x = Ax + NX;
     MPCQP_STAMP_INIT(tst);
 
@@ -163,8 +173,8 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     C.nfmax = NF;
     C.L.ld = LD;
     C.L.R = D + Lay::oR;
-    C.L.J = D + Lay::oJ;
-    C.L.g = D + Lay::oG;
+    C.L.J = nullptr;
+    C.L.g = nullptr;
     C.L.xs = D + Lay::oXS;
     C.L.xfull = D + Lay::oXF;
     C.L.rowfix = D + Lay::oMisc;
@@ -233,7 +243,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     const double Ts = a.Ts;
     // [Ac | Bc] into LDS once, lane i writing row i with compile-time columns (the R space is
     // free until H_FF is built there); the products then read it
-    double *T = C.L.R;
+    double *T = D + Lay::oT;
     if (ln < NX) {
 #pragma unroll
         for (int j = 0; j < NS; ++j) T[j * NX + ln] = entry(ln, j);
@@ -268,14 +278,14 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     MPCQP_STAMP(a.stamps, 0, tst);
     MPCQP_CUT(a.cut, 1);
 
-    // ---- S^W_rr = X_r' W X_r over the support rows (w: 0 = Q, 1 = P); slot rs = 4w + 3r of
-    //      entry o = cj NU + ci (the cross blocks rs = 1, 2, 5, 6 are zero and never read).
+    // ---- S^W_rr = X_r' W X_r over the support rows (w: 0 = Q, 1 = P); slot blk = 2w + r of
+    //      entry o = cj NU + ci (the cross blocks X0' W X1 are zero and not stored).
     //      The block loop is wave-uniform so the weights are scalar loads.
     using Sup = XSupport<MODEL>;
     constexpr int SD = Sup::x0hi - Sup::x0lo;
 #pragma unroll
     for (int blk = 0; blk < 4; ++blk) {
-        const int r_ = blk & 1, w_ = blk >> 1, rs = 4 * w_ + 3 * r_;
+        const int r_ = blk & 1, w_ = blk >> 1;
         const int lo = r_ ? Sup::x1lo : Sup::x0lo;
         const double *Xr = r_ ? X1 : X0;
         const double *w = w_ ? a.pd : a.qd;
@@ -284,7 +294,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
             double acc = 0.0;
 #pragma unroll
             for (int l = lo; l < lo + SD; ++l) acc += Xr[ci * NX + l] * w[l] * Xr[cj * NX + l];
-            S[e * 8 + rs] = acc;  // [o = cj NU + ci][rs]: one entry's terms contiguous
+            S[e * 4 + blk] = acc;  // [o = cj NU + ci][blk]: one entry's terms contiguous
         }
     }
     // ---- u_m(c) = X0[:,c]' W_m e_m, v_m(c) = X1[:,c]' W_m e_m, m = 1..N (support rows only)
@@ -316,10 +326,10 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
         double c, si, sj, sij;
         beta_sums(kk + 1, N - 1, ki, kj, c, si, sj, sij);
         const double bi = (double)(N - 1 - ki) + 0.5, bj = (double)(N - 1 - kj) + 0.5;
-        const double *So = S + (cj * NU + ci) * 8;  // cross blocks are zero (XSupport)
+        const double *So = S + (cj * NU + ci) * 4;  // cross blocks are zero (XSupport)
         (void)si; (void)sj;
-        double v = c * So[0] + sij * So[3];
-        v += So[4] + bi * bj * So[7];
+        double v = c * So[0] + sij * So[1];
+        v += So[2] + bi * bj * So[3];
         if (ki == kj) v += D[Lay::oRm + cj * NU + ci];
         return 2.0 * v;
     };
@@ -362,9 +372,9 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
                     for (int rj = mj; rj; rj &= rj - 1) {
                         const int cj = __builtin_ctz(rj), qq = pos[kj * NU + cj];
                         if (pp >= qq) {
-                            const double *So = S + (cj * NU + ci) * 8;
-                            double v = c * So[0] + sij * So[3];  // cross blocks zero
-                            v += So[4] + bij * So[7];
+                            const double *So = S + (cj * NU + ci) * 4;
+                            double v = c * So[0] + sij * So[1];  // cross blocks zero
+                            v += So[2] + bij * So[3];
                             if (ki == kj) v += D[Lay::oRm + cj * NU + ci];
                             Hb[lrow(pp) + qq] = 2.0 * v;
                         }
@@ -385,22 +395,6 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
         MPCQP_STAMP(a.stamps, 3, tst);
         MPCQP_CUT(a.cut, 3);
         gi_run_reg<NF>(C, h, gp, D + Lay::oRow);
-    } else {
-        if (ok) {
-            const int E = nf * (nf + 1) / 2;
-            for (int e = ln; e < E; e += kWave) {
-                int p = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-                while (p * (p + 1) / 2 > e) --p;
-                while ((p + 1) * (p + 2) / 2 <= e) ++p;
-                const int q = e - p * (p + 1) / 2;
-                C.L.R[q * LD + p] = H_entry(C.L.fid[p], C.L.fid[q]);
-            }
-            if (ln < nf) C.L.g[ln] = gp;
-        }
-        wave_sync();
-        MPCQP_STAMP(a.stamps, 3, tst);
-        MPCQP_CUT(a.cut, 3);
-        gi_run(C);
     }
 #ifdef MPCQP_CUTS
     if (a.cut >= 4 && a.cut <= 7) return;

@@ -21,6 +21,10 @@
 #include <new>
 
 #include "../../include/mpcqp.h"
+
+#ifndef MPCQP_W32
+#define MPCQP_W32 3  // waves per SIMD the NF <= 32 fused kernel is register-budgeted for
+#endif
 #include "condense.hpp"
 #include "fused.hpp"
 #include "mpc_fused.hpp"
@@ -354,7 +358,7 @@ __global__ void __launch_bounds__(64) k_condense_solve(FastArgs a) {
 }
 
 template <int NU, int N, int MODEL, bool FRIC, int NF>
-__global__ void __launch_bounds__(64, (NF <= 32 ? 3 : 2)) k_mpc(MpcArgs a) {
+__global__ void __launch_bounds__(64, (NF <= 32 ? MPCQP_W32 : 2)) k_mpc(MpcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_m[];
     if ((int)blockIdx.x >= a.B) return;
     fast_mpc<NU, N, MODEL, FRIC, NF>(a, smem_m);

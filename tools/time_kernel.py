@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""Median k_mpc time over repeated launches for a config (library from $MPCQP_LIB)."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mpc-limx-control_amd"))
+import numpy as np  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--configs", default="B,C,L")
+ap.add_argument("--batch", type=int, default=65536)
+ap.add_argument("--reps", type=int, default=20)
+args = ap.parse_args()
+import mpcqp  # noqa: E402
+from mpcqp.engine import BatchEngine  # noqa: E402
+print("lib", os.environ.get("MPCQP_LIB", "default"))
+for cfg in args.configs.split(","):
+    p = mpcqp.model_params(cfg)
+    eng = BatchEngine(p)
+    d = eng.upload(mpcqp.make_batch(p, args.batch))
+    eng.enable_timing(True)
+    ts = []
+    for r in range(args.reps + 3):
+        eng.solve(d)
+        eng.sync()
+        if r >= 3:
+            ts.append(eng.last_kernel_ms(1))
+    st = d["status"].cpu().numpy()
+    print(f"  {cfg}: {np.median(ts):.4f} ms  ({args.batch / np.median(ts) / 1e3:.2f} M QP/s)  "
+          f"solved {np.mean(st == 0):.4f}")
+    eng.close()
