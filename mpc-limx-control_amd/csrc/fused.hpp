@@ -139,6 +139,7 @@ __device__ __forceinline__ void fast_condense_solve(const FastArgs &a, unsigned 
     C.L.fid = ip;
     C.L.pos = ip + NFMAX;
     C.L.st = reinterpret_cast<unsigned char *>(ip + NFMAX + NV);
+    C.L.cb = nullptr;
 
     // ---- inputs
     const double *ABg = a.AB + (size_t)b * NX * NS;

@@ -57,7 +57,7 @@ __device__ __forceinline__ void gi_project_reg(const GiCtx &C, const double (&Jr
     const SolveProblem &P = *C.P;
     const GiLds &L = C.L;
     const int nf = C.nf, nfric = C.nfric, ln = lane();
-    const double b = gi_cons_b(C, id);
+    const double b = id < 2 * nf ? L.cb[id] : gi_cons_b(C, id);
     if (id < 2 * nf) {
         const int a = id < nf ? id : id - nf;
         const double sg = id < nf ? 1.0 : -1.0;
@@ -87,8 +87,8 @@ __device__ __forceinline__ void gi_project_reg(const GiCtx &C, const double (&Jr
 }
 
 // h: lane p holds row p of H_FF (columns < nf meaningful), g: lane p holds g_p.
-// rowbuf: 4 NF doubles of LDS (16-byte aligned): row / column broadcast buffers and the
-// rotation pairs.  Broadcasts go through LDS (one ds_read_b128 brings two values to every
+// rowbuf: 5 NF doubles of LDS (16-byte aligned): row / column broadcast buffers, the
+// rotation pairs and 1/R(j,j).  Broadcasts go through LDS (one ds_read_b128 brings two values to every
 // lane) rather than v_readlane pairs, which cost VALU issue slots.  Fills C.{status,x,u,fval,act,q,iters}.
 template <int NF>
 __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, double *rowbuf) {
@@ -103,7 +103,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
     constexpr bool T63 = NF < kWave;  // lane 63 computes t = L^-1 g in the inverse sweep
     double gv = g;     // lane i: g_i, then t_i = (L^-1 g)_i (fused path, NF == 64)
     double dinv = 1.0; // lane i: 1 / L(i,i) (fused path)
-    double *colb = rowbuf + NF, *rot = rowbuf + 2 * NF;
+    double *colb = rowbuf + NF, *rot = rowbuf + 2 * NF, *rinv = rowbuf + 4 * NF;
     MPCQP_STAMP_INIT(tst);
 
     if (status == ST_OK && nf > 0) {
@@ -228,8 +228,11 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             int bid = 0x7fffffff;
             for (int id = ln; id < mt; id += kWave) {
                 if (L.st[id] != 1) continue;
-                const double sl_ = gi_cons_slack_lane(C, id);
-                if (sl_ < -kFeasTol * (1.0 + fabs(gi_cons_b(C, id))) && sl_ < best) { best = sl_; bid = id; }
+                double b, sl_;
+                if (id < nf) { b = L.cb[id]; sl_ = L.xs[id] - b; }
+                else if (id < 2 * nf) { b = L.cb[id]; sl_ = -L.xs[id - nf] - b; }
+                else { b = gi_cons_b(C, id); sl_ = gi_cons_slack_lane(C, id); }  // friction
+                if (sl_ < -kFeasTol * (1.0 + fabs(b)) && sl_ < best) { best = sl_; bid = id; }
             }
             wave_argmin(best, bid);
             if (bid == 0x7fffffff) break;  // optimal
@@ -254,18 +257,20 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             if ((j & 7) == 7) step_fence();
         }
         const double z = (z4[0] + z4[1]) + (z4[2] + z4[3]);
-        // r = R^-1 d(0:q) (R in LDS)
-        double r = 0.0, val = dj;
-        for (int j = q - 1; j >= 0; --j) {
-            const double rj = readlane(val, j) / L.R[roff(j) + j];
-            if (ln == j) r = rj;
-            if (ln < j) val -= L.R[roff(j) + ln] * rj;
-        }
-        const double rmax = wave_max(ln < q ? fabs(r) : 0.0);
-        double t1 = INFINITY;
+        // r = R^-1 d(0:q) (R in LDS, 1/R(j,j) kept beside it); nothing to do while q == 0
+        double r = 0.0, t1 = INFINITY;
         int kslot = 0x7fffffff;
-        if (ln < q && r > kRTol * rmax) { t1 = u / r; kslot = ln; }
-        wave_argmin(t1, kslot);
+        if (q > 0) {
+            double val = dj;
+            for (int j = q - 1; j >= 0; --j) {
+                const double rj = readlane(val, j) * rinv[j];
+                if (ln == j) r = rj;
+                if (ln < j) val -= L.R[roff(j) + ln] * rj;
+            }
+            const double rmax = wave_max(ln < q ? fabs(r) : 0.0);
+            if (ln < q && r > kRTol * rmax) { t1 = u / r; kslot = ln; }
+            wave_argmin(t1, kslot);
+        }
         const bool dep = !(zn > kDepTol * dd);
         const double t2 = dep ? INFINITY : -sp / zn;
         const double t = t1 < t2 ? t1 : t2;
@@ -302,7 +307,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             if (ln < NF) { rot[2 * ln] = cl; rot[2 * ln + 1] = sl; }
             const double rqq = readlane(accl, q);
             if (ln < q) L.R[roff(q) + ln] = dj;
-            if (ln == q) { L.R[roff(q) + q] = rqq; act = p; }
+            if (ln == q) { L.R[roff(q) + q] = rqq; rinv[q] = 1.0 / rqq; act = p; }
             if (ln == 0) L.st[p] = 2;
             ++q;
             fresh = true;
@@ -341,9 +346,13 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                     if (ln == 0) {
                         L.R[roff(j) + j] = hh;
                         L.R[roff(j) + j + 1] = 0.0;
+                        rinv[j] = ih;
                         rot[2 * j] = c;
                         rot[2 * j + 1] = s_;
                     }
+                    wave_sync();
+                } else {
+                    if (ln == 0) rinv[j] = 1.0 / a;  // the shifted column's diagonal as it is
                     wave_sync();
                 }
             }

@@ -76,6 +76,7 @@ __host__ __device__ inline size_t gi_lds_bytes(int nfmax, int nV, int mA, int nf
 
 struct GiLds {
     double *J, *R, *g, *xs, *xfull, *rowfix, *ys;
+    double *cb;  // nullable: b of every constraint id, precomputed by gi_setup (register solver)
     int *fid, *pos;
     unsigned char *st;  // 0 absent, 1 inactive, 2 active, 3 equality, 4 infeasible
     int ld;
@@ -96,6 +97,7 @@ __device__ __forceinline__ GiLds gi_carve(unsigned char *base, int nfmax, int nV
     L.fid = ip; ip += nfmax;
     L.pos = ip; ip += nV;
     L.st = reinterpret_cast<unsigned char *>(ip);
+    L.cb = nullptr;
     return L;
 }
 
@@ -296,6 +298,10 @@ __device__ __forceinline__ void gi_setup(GiCtx &C) {
     bool infe = false;
     for (int id = ln; id < mt; id += kWave) infe |= (L.st[id] == 4);
     if (__any(infe)) C.status = ST_INFEASIBLE;
+    if (L.cb) {  // b of the bound constraints, once (the dual loop's sweeps read it)
+        for (int id = ln; id < 2 * nf; id += kWave) L.cb[id] = gi_cons_b(C, id);
+        wave_sync();
+    }
 }
 
 // ---------------------------------------------------------------- stage 2: gather

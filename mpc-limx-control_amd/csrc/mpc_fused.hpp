@@ -92,19 +92,18 @@ struct MpcLayout {
     static constexpr int MT = 2 * NF + NFRIC;
     static constexpr bool REG = true;
     static constexpr int NR = RegPack<NF>::doubles;  // packed L / R
-    // doubles.  Live for the whole kernel: S (4 nonzero blocks, entry-major), u/v, R copy,
-    // x mirror, fixed values; then one region the phases take turns on:
-    //   model/condensing: T = [Ac | Bc] (scratch), X0, X1, A x0, A^2 x0, xref, x0
-    //   H_FF build      : packed H (first nf(nf+1)/2 doubles)
-    //   solver          : packed L / R, then the 4 NF broadcast buffers
-    static constexpr int oS = 0;                          // [NU*NU][4]
-    static constexpr int oUV = oS + 4 * NU * NU;          // u_m, v_m: [(N+1)][2][NU]
-    static constexpr int oRm = oUV + (N + 1) * 2 * NU;    // R (NU x NU) copy
-    static constexpr int oXS = oRm + NU * NU;             // x mirror (NF)
+    // doubles.  Live for the whole kernel: the x mirror, fixed values, the bounds' b; then one
+    // region the phases take turns on (relative offsets):
+    //   model/condensing : T = [Ac | Bc] (scratch), X0, X1, A x0, A^2 x0, xref, x0 at [0, E)
+    //   condensed terms  : S (4 nonzero blocks, entry-major), u/v, R copy at [max(E, HB), ..)
+    //   H_FF build       : packed H at [0, HB), HB = NF(NF+1)/2, reading the condensed terms
+    //   solver           : packed L / R at [0, NR), then 5 NF broadcast / 1/R(j,j) doubles
+    static constexpr int oXS = 0;                         // x mirror (NF)
     static constexpr int oXF = oXS + NF;                  // xfull (NV)
     static constexpr int oMisc = oXF + NV;                // rowfix / ys slot
-    static constexpr int oU = (oMisc + 2 + 1) & ~1;       // the shared region (16-B aligned)
-    // early-phase view of the shared region
+    static constexpr int oCB = oMisc + 2;                 // b of the bound constraints (2 NF)
+    static constexpr int oU = (oCB + 2 * NF + 1) & ~1;    // the shared region (16-B aligned)
+    // early-phase view
     static constexpr int oT = oU;                         // [Ac | Bc] (NX x (NX+NU))
     static constexpr int oX0 = oT + NX * (NX + NU);       // B  (NX x NU)
     static constexpr int oX1 = oX0 + NX * NU;             // AB (NX x NU)
@@ -112,16 +111,23 @@ struct MpcLayout {
     static constexpr int oXr = oAx + 2 * NX;              // xref (NX x (N+1))
     static constexpr int oX0v = oXr + NX * (N + 1);       // x0 (NX)
     static constexpr int nEarly = oX0v + NX + 1 - oU;
+    static constexpr int HB = NF * (NF + 1) / 2;
+    // condensed terms, live until H_FF and g are built
+    static constexpr int oS = oU + (((nEarly > HB ? nEarly : HB) + 1) & ~1);  // [NU*NU][4]
+    static constexpr int oUV = oS + 4 * NU * NU;          // u_m, v_m: [(N+1)][2][NU]
+    static constexpr int oRm = oUV + (N + 1) * 2 * NU;    // R (NU x NU) copy
+    static constexpr int nMid = oRm + NU * NU - oU;
     // solver view
     static constexpr int oR = oU;                         // packed L / R (and H_FF before)
-    static constexpr int oRow = (oR + NR + 1) & ~1;       // broadcast buffers (4 NF)
-    static constexpr int nLate = oRow + 4 * NF - oU;
-    static constexpr int nDoubles = oU + (nEarly > nLate ? nEarly : nLate);
+    static constexpr int oRow = (oR + NR + 1) & ~1;       // broadcast buffers (4 NF) + 1/R(j,j)
+    static constexpr int nLate = oRow + 5 * NF - oU;
+    static constexpr int nShared = nMid > nLate ? nMid : nLate;
+    static constexpr int nDoubles = oU + nShared;
     static constexpr size_t bytes =
         sizeof(double) * nDoubles + sizeof(int) * (NF + NV) + ((MT + 15) & ~15);
     static constexpr size_t lds_bytes = (bytes + 15) & ~(size_t)15;
-    static_assert(oRow % 2 == 0 && oU % 2 == 0, "16-byte aligned buffers");
-    static_assert(NF * (NF + 1) / 2 <= NR, "packed H fits the L / R space");
+    static_assert(oRow % 2 == 0 && oU % 2 == 0 && oS % 2 == 0, "16-byte aligned buffers");
+    static_assert(HB <= NR, "packed H fits the L / R space");
 };
 
 // sum over m in [m0, m1] of 1, beta_i, beta_j, beta_i beta_j; beta_x = m - 1 - k_x + 1/2
@@ -183,6 +189,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     C.L.fid = ip;
     C.L.pos = ip + NF;
     C.L.st = reinterpret_cast<unsigned char *>(ip + NF + NV);
+    C.L.cb = D + Lay::oCB;
 
     // ---- per-instance inputs: all global loads issued back to back (one HBM round trip),
     //      then parked in LDS
