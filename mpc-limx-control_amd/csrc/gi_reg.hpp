@@ -22,9 +22,15 @@ namespace mpcqp {
 __device__ __forceinline__ int roff(int j) { return j * (j + 3) / 2; }
 // packed L (parked for the inverse): row i holds columns 0..i
 __host__ __device__ constexpr int lrow(int i) { return i * (i + 1) / 2; }
+// column-major packed L kept during the factorisation: column k holds rows k..NF-1 and
+// starts 16-byte aligned (two doubles)
+__host__ __device__ constexpr int ccol(int k, int nf) {
+    return k == 0 ? 0 : ccol(k - 1, nf) + ((nf - (k - 1) + 1) & ~1);
+}
 template <int NF>
 struct RegPack {
     static constexpr int doubles = NF * (NF + 3) / 2;  // >= lrow(NF): L fits in R's space
+    static_assert(ccol(NF, NF) <= doubles, "column-packed L fits the R space");
 };
 
 // Row-broadcast of J: d_j = c0 J(a0, j) [+ c1 J(a1, j)] on lane j.  The owning lanes publish
@@ -102,8 +108,8 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
     double Jr[NF];
     constexpr bool T63 = NF < kWave;  // lane 63 computes t = L^-1 g in the inverse sweep
     double gv = g;     // lane i: g_i, then t_i = (L^-1 g)_i (fused path, NF == 64)
-    double dinv = 1.0; // lane i: 1 / L(i,i) (fused path)
     double *colb = rowbuf + NF, *rot = rowbuf + 2 * NF, *rinv = rowbuf + 4 * NF;
+    double *Lc = L.R;  // column-packed L (the R space is free until the dual loop)
     MPCQP_STAMP_INIT(tst);
 
     if (status == ST_OK && nf > 0) {
@@ -125,9 +131,11 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             if constexpr (!T63) {
                 const double tk = readlane(gv, k) * ik;
                 gv = (ln == k) ? tk : ((ln > k) ? gv - lik * tk : gv);
-                dinv = (ln == k) ? ik : dinv;
             }
-            if (ln > k && ln < NF) colb[ln] = lik;  // column k of L, broadcast through LDS
+            // column k of L (diagonal first) into LDS: the broadcast for this step's update
+            // and, kept, the operand of the inverse sweep; 1/L(k,k) beside it
+            if (ln >= k && ln < NF) Lc[ccol(k, NF) + ln - k] = lik;
+            if (ln == 0) rowbuf[k] = ik;
             double pivn = 1.0, ikn = 1.0;
             if (k + 1 < NF) {
                 pivn = readlane(h[k + 1 < NF ? k + 1 : k] - lik * lik, k + 1);
@@ -138,16 +146,13 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
 #pragma unroll
             for (int j = 0; j < NF; ++j)
             {
-                if (j > k) h[j] -= lik * colb[j];
+                if (j > k) h[j] -= lik * Lc[ccol(k, NF) + j - k];
                 if ((j & 7) == 7 && j > k) step_fence();  // bound the loads in flight
             }
 #pragma unroll
             for (int j = 0; j < NF; ++j)
                 if (j >= k) pin(h[j]);  // step k's updates happen in step k
-            if constexpr (!T63) {
-                pin(gv);
-                pin(dinv);
-            }
+            if constexpr (!T63) pin(gv);
             piv = pivn;
             ik = ikn;
             pin(piv);
@@ -158,34 +163,30 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
     }
     MPCQP_STAMP(C.stamps, 5, tst); MPCQP_CUT(C.cut, 4);
     if (status == ST_OK && nf > 0) {
-        // ---- park L in the (still empty) R space, row i at lrow(i); 1/L(i,i) in rowbuf
-        double *Lp = L.R;
-        if (ln < NF) {
-#pragma unroll
-            for (int l = 0; l < NF; ++l)
-                if (l <= ln) Lp[lrow(ln) + l] = h[l];
-            if constexpr (!T63) rowbuf[ln] = dinv;
-        }
+        // ---- columns of L^-1, right-looking: lane c solves L y = e_c (lane 63: L t = g when
+        //      NF < 64) column by column of L, whose entries are uniform-address LDS
+        //      broadcasts; a step's updates are independent FMAs.  y = column c of L^-1 =
+        //      row c of J, kept in registers.  Lanes >= NF start from 0 and stay 0.
         if constexpr (T63) {
-            if (ln < NF) colb[ln] = gv;  // g, read by lane 63 as its right-hand side
-            wave_sync();
-            if (ln < NF) rowbuf[ln] = 1.0 / Lp[lrow(ln) + ln];
+            if (ln < NF) colb[ln] = gv;  // g, the right-hand side of lane 63
         }
         wave_sync();
-        // ---- columns of L^-1 (lane c); L(i,l) are uniform-address LDS broadcasts, so only
-        //      J occupies registers here.  Lanes >= NF start from 0 and stay 0.
+#pragma unroll
+        for (int l = 0; l < NF; ++l) {
+            Jr[l] = (ln == l) ? 1.0 : 0.0;
+            if constexpr (T63) Jr[l] = (ln == kWave - 1) ? colb[l] : Jr[l];
+        }
 #pragma unroll
         for (int i = 0; i < NF; ++i) {
-            // four partial sums: the dot product is an FMA-latency chain otherwise
-            double s4[4] = {(ln == i) ? 1.0 : 0.0, 0.0, 0.0, 0.0};
-            if constexpr (T63) s4[0] = (ln == kWave - 1) ? colb[i] : s4[0];
+            Jr[i] *= rowbuf[i];
 #pragma unroll
             for (int l = 0; l < NF; ++l) {
-                if (l < i) s4[l & 3] -= Lp[lrow(i) + l] * Jr[l];
-                if ((l & 15) == 15 && l < i) step_fence();  // bound the loads in flight
+                if (l > i) Jr[l] -= Lc[ccol(i, NF) + l - i] * Jr[i];
+                if ((l & 15) == 15 && l > i) step_fence();  // bound the loads in flight
             }
-            Jr[i] = ((s4[0] + s4[1]) + (s4[2] + s4[3])) * rowbuf[i];
-            pin(Jr[i]);
+#pragma unroll
+            for (int l = 0; l < NF; ++l)
+                if (l >= i) pin(Jr[l]);
             step_fence();  // keep step i's loads and arithmetic in step i
         }
         MPCQP_STAMP(C.stamps, 6, tst); MPCQP_CUT(C.cut, 5);
