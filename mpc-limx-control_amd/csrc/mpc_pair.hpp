@@ -1,0 +1,638 @@
+// mpc_pair.hpp -- the fused per-tick step of mpc_fused.hpp with TWO QP instances per
+// wavefront: lanes 0-31 own instance 2w, lanes 32-63 instance 2w+1.
+//
+// Reference: mpcQP::mpcQP + buildSystemModel (include/mpcQP.h:35-119, 121-182),
+// QPSolver::discretizeSystem / buildQPParams / solveQP (src/QPSolver.cpp:21-106).
+//
+// For problems with at most 31 free variables -- config B (SRBM 13/6/10: the gait has one
+// stance foot per horizon step, nf = 30) and the reference-literal 13/3/10 model (nf = 30) --
+// the one-QP-per-wave kernel leaves lanes 32-63 idle through the factorisation, the inverse
+// and the dual loop, and an FP64 wave instruction costs 4 cycles however many lanes it uses.
+// Here every lane-parallel phase serves two instances for the same instruction count:
+//   * lane l of a half owns row l of H_FF / L and row l of J (31 columns in registers); lane
+//     31 of each half carries g through the inverse sweep (t = L^-1 g), as lane 63 does in
+//     gi_reg.hpp
+//   * broadcasts are LDS reads at a per-half address (one address per half); cross-lane reads
+//     at a uniform index are v_readlane of both halves plus a select (wave_ops.hpp, half_*)
+//   * reductions: DPP inside each 16-lane row, then the half's two rows
+//   * the dual loop runs while either half is active; each half's state (q, iterations,
+//     status, the selected constraint) lives in VGPRs and a finished half idles (EXEC-masked)
+// Same algorithm, constraint order, tolerances and arithmetic as fast_mpc + gi_run_reg, so
+// results and iteration counts match the one-QP kernel and the CPU oracle.
+//
+// LDS per instance (config B): 6.2 KB -- the early model terms keep only the support rows of
+// X0 / X1 and no [Ac | Bc] copy, the condensed linear terms die before the packed H is built
+// over them, and the bounds' b are recomputed from the free map -- so three waves (six QPs)
+// per SIMD fit in 160 KB.
+#pragma once
+#include "mpc_fused.hpp"
+
+namespace mpcqp {
+
+constexpr int kPairNF = 31;  // free variables per instance; lane 31 of a half carries g
+
+template <int NU, int N, int MODEL>
+struct PairLayout {
+    static constexpr int NX = 13, NF = kPairNF, NV = NU * N, MT = 2 * NF, NP = kHalf;
+    using Sup = XSupport<MODEL>;
+    static constexpr int SD = Sup::x0hi - Sup::x0lo;
+    static constexpr int NR = RegPack<NF>::doubles;  // packed L / R
+    static constexpr int HB = NF * (NF + 1) / 2;     // packed H_FF
+    // doubles.  Live for the whole kernel: the x mirror.  Then one region, in turn:
+    //   early   : X0, X1 support rows, A x0, A^2 x0, xref, x0, then u_m / v_m   [oU, eUV)
+    //   H build : packed H [oU, oU + HB) over the dead early view; S and the R copy after it
+    //   solver  : packed L / R [oU, oU + NR), then 5 x 32 broadcast doubles
+    static constexpr int oXS = 0;
+    static constexpr int oU = NP;
+    static constexpr int oX0 = oU;                       // [NU][SD]
+    static constexpr int oX1 = oX0 + NU * SD;            // [NU][SD]
+    static constexpr int oAx = oX1 + NU * SD;            // NX
+    static constexpr int oA2x = oAx + NX;                // NX
+    static constexpr int oXr = oA2x + NX;                // NX (N+1), Eigen column-major
+    static constexpr int oX0v = oXr + NX * (N + 1);      // NX
+    static constexpr int oUV = oX0v + NX;                // [(N+1)][2][NU]
+    static constexpr int eUV = oUV + (N + 1) * 2 * NU;
+    static constexpr int oS = oU + ((HB > eUV - oU ? HB : eUV - oU) + 1) / 2 * 2;  // [NU*NU][4]
+    static constexpr int oRm = oS + 4 * NU * NU;         // R (NU x NU)
+    static constexpr int eMid = oRm + NU * NU;
+    static constexpr int oR = oU;
+    static constexpr int oRow = (oR + NR + 1) & ~1;      // buf | colb | rot (2 NP) | 1/R(j,j)
+    static constexpr int eLate = oRow + 5 * NP;
+    static constexpr int nDoubles = ((eMid > eLate ? eMid : eLate) + 1) & ~1;
+    static constexpr size_t bytes =
+        (sizeof(double) * nDoubles + sizeof(int) * (NF + NV) + ((MT + 15) & ~15) + 15) & ~(size_t)15;
+    static constexpr size_t lds_bytes = 2 * bytes;  // both halves
+    static_assert(oU % 2 == 0 && oRow % 2 == 0 && oS % 2 == 0, "16-byte aligned buffers");
+    static_assert(HB <= NR, "packed H fits the L / R space");
+    static_assert(N <= kHalf, "one lane per horizon step in the gait mask");
+};
+
+// bounds of variable v from the contact schedule (gen_bound, gi_solver.hpp)
+template <int NU, int MODEL>
+__device__ __forceinline__ void pair_bound(const MpcArgs &a, uint64_t contact, int v, double &lo,
+                                           double &hi) {
+    if (MODEL == 1) { lo = a.u_min; hi = a.u_max; return; }
+    const int k = v / NU, c = v % NU, s = c / 3, comp = c % 3;
+    if ((contact >> (2 * k + s)) & 1ull) {
+        if (comp == 2) { lo = a.fz_min; hi = a.fz_max; }
+        else { lo = -a.fxy_max; hi = a.fxy_max; }
+    } else { lo = 0.0; hi = 0.0; }
+}
+// b of the one-sided bound constraint on FREE variable v (a free SRBM force is in contact):
+// lower x >= lo (b = lo), upper -x >= -hi (b = -hi) -- gi_cons_b without the LDS table
+template <int NU, int MODEL>
+__device__ __forceinline__ double pair_free_b(const MpcArgs &a, int v, bool upper) {
+    if (MODEL == 1) return upper ? -a.u_max : a.u_min;
+    const bool z = (v % NU) % 3 == 2;
+    return upper ? -(z ? a.fz_max : a.fxy_max) : (z ? a.fz_min : -a.fxy_max);
+}
+
+// gait_mask_wave per half: lane l < N of each half evaluates step l of its own instance
+__device__ __forceinline__ uint64_t gait_mask_half(int N, double Ts, double phase0, float swing,
+                                                   float stance) {
+    const double cycle = (double)(swing + stance), sw = (double)swing;
+    const int hl = lane() & (kHalf - 1);
+    const double ph = fmod(phase0 + (double)hl * Ts, cycle);
+    const uint64_t right = half_ballot(hl < N && ph < sw);
+    const uint64_t left = half_ballot(hl < N && !(ph < sw));
+    return spread_even(left) | (spread_even(right) << 1);
+}
+
+template <int NU, int N, int MODEL, bool GEN>
+__device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) {
+    static_assert(!GEN || MODEL == 0, "generated inputs are defined for the SRBM model");
+    static_assert(MODEL == 0 || MODEL == 1, "TRON1 models only");
+    using Lay = PairLayout<NU, N, MODEL>;
+    using Sup = XSupport<MODEL>;
+    constexpr int NX = 13, NS = NX + NU, NF = kPairNF, NV = Lay::NV, SD = Lay::SD, NP = kHalf;
+    const int ln = lane(), hl = ln & (kHalf - 1);
+    const bool up = ln >= kHalf;
+    const int bq = 2 * (int)blockIdx.x + (up ? 1 : 0);
+    const bool valid = bq < a.B;
+    const int b = valid ? bq : a.B - 1;  // the spare half of an odd batch re-reads the last QP
+    double *D = reinterpret_cast<double *>(smem + (up ? Lay::bytes : 0));
+    double *xs = D + Lay::oXS;
+    int *fid = reinterpret_cast<int *>(D + Lay::nDoubles);
+    int *pos = fid + NF;
+    unsigned char *st = reinterpret_cast<unsigned char *>(pos + NV);
+    double *X0 = D + Lay::oX0, *X1 = D + Lay::oX1, *Ax = D + Lay::oAx, *A2x = D + Lay::oA2x;
+    double *xr = D + Lay::oXr, *x0g = D + Lay::oX0v, *UV = D + Lay::oUV;
+    double *S = D + Lay::oS, *Rm = D + Lay::oRm;
+
+    // ---- per-instance inputs: all global loads back to back, then parked in LDS
+    double lin[8];
+    uint64_t contact = 0;
+    constexpr int NRM = NU * NU;
+    if constexpr (GEN) {
+        // x0 = the state; xref as mpcQP::mpcQP builds it (include/mpcQP.h:74-97)
+        const int s_ = b / a.cands;
+        const double stv = (hl < NX) ? a.state[(size_t)s_ * NX + hl] : 0.0;
+        const double wz = a.cmd[(size_t)s_ * 2], vx = a.cmd[(size_t)s_ * 2 + 1];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) lin[1 + i] = a.feet[(size_t)s_ * 6 + i];
+        lin[7] = 0.0;
+        const double ph0 = a.phase[b];
+        const double rm0 = (hl < NRM) ? a.rmat[hl] : 0.0;
+        const double rm1 = (hl + kHalf < NRM) ? a.rmat[hl + kHalf] : 0.0;
+        if (hl < NX) x0g[hl] = stv;
+        if (hl < NRM) Rm[hl] = rm0;
+        if (hl + kHalf < NRM) Rm[hl + kHalf] = rm1;
+        lin[0] = hread(stv, 2);
+        if (hl < NX) {
+#pragma unroll
+            for (int i = 0; i <= N; ++i) {
+                const double t = (double)i * a.Ts;
+                double v = stv;
+                if (hl == 2) v = stv + t * wz;
+                if (hl == 3) v = stv + t * vx;
+                if (hl == 9 && i > 0) v = vx;
+                if (hl == 12) v = -9.8;
+                xr[i * NX + hl] = v;
+            }
+        }
+        contact = gait_mask_half(N, a.Ts, ph0, a.swing, a.stance);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) lin[i] = a.lin[(size_t)b * 8 + i];
+        constexpr int NXR = NX * (N + 1), RX = (NXR + kHalf - 1) / kHalf;
+        const double *xrg = a.xref + (size_t)b * NXR;
+        double v[RX];
+#pragma unroll
+        for (int r = 0; r < RX; ++r) v[r] = (hl + r * kHalf < NXR) ? xrg[hl + r * kHalf] : 0.0;
+        const double x0l = (hl < NX) ? a.x0[(size_t)b * NX + hl] : 0.0;
+        const double rm0 = (hl < NRM) ? a.rmat[hl] : 0.0;
+        const double rm1 = (hl + kHalf < NRM) ? a.rmat[hl + kHalf] : 0.0;
+        if (MODEL == 0) contact = a.contact[b];
+#pragma unroll
+        for (int r = 0; r < RX; ++r)
+            if (hl + r * kHalf < NXR) xr[hl + r * kHalf] = v[r];
+        if (hl < NX) x0g[hl] = x0l;
+        if (hl < NRM) Rm[hl] = rm0;
+        if (hl + kHalf < NRM) Rm[hl + kHalf] = rm1;
+    }
+    wave_sync();
+
+    // ---- model: lane i < NX holds row i of Ac; X0 = Bc Ts and X1 = (Ac Ts) X0 on their
+    //      support rows, A x0, A^2 x0 (A = Ac Ts).  Same products, in the same order, as the
+    //      one-QP kernel (the zero terms it adds are exact).
+    double Iwi[9];
+    double cy = 1.0, sy = 0.0;
+    if (MODEL == 0) srbm_rot_inertia(lin[0], a.Ibinv, cy, sy, Iwi);
+    auto entry = [&](int i, int j) -> double {  // [Ac | Bc](i, j)
+        return MODEL == 0 ? srbm_entry(i, j, lin, cy, sy, Iwi, a.mass)
+                          : literal_entry(i, j, lin, a.mass);
+    };
+    const double Ts = a.Ts;
+    double arow[NX];
+#pragma unroll
+    for (int k = 0; k < NX; ++k) arow[k] = entry(hl, k);
+    if (hl >= Sup::x0lo && hl < Sup::x0hi) {
+#pragma unroll
+        for (int c = 0; c < NU; ++c) X0[c * SD + hl - Sup::x0lo] = entry(hl, NX + c) * Ts;
+    }
+    if (hl < NX) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < NX; ++k) s += arow[k] * x0g[k];
+        Ax[hl] = s * Ts;
+    }
+    wave_sync();
+    if (hl >= Sup::x1lo && hl < Sup::x1hi) {
+#pragma unroll
+        for (int c = 0; c < NU; ++c) {
+            double s = 0.0;
+#pragma unroll
+            for (int k = Sup::x0lo; k < Sup::x0hi; ++k) s += arow[k] * X0[c * SD + k - Sup::x0lo];
+            X1[c * SD + hl - Sup::x1lo] = s * Ts;
+        }
+    }
+    if (hl < NX) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < NX; ++k) s += arow[k] * Ax[k];
+        A2x[hl] = s * Ts;
+    }
+
+    // ---- free map and constraint states (gi_setup for generated bounds, no rows)
+    int status = ST_OK, nf = 0;
+    {
+        bool infeas = false;
+#pragma unroll
+        for (int base = 0; base < NV; base += kHalf) {
+            const int v = base + hl;
+            const bool vv = v < NV;
+            double lo = -kInfty, hi = kInfty;
+            if (vv) pair_bound<NU, MODEL>(a, contact, v, lo, hi);
+            const bool freev = vv && lo != hi;
+            infeas |= half_ballot(vv && lo > hi) != 0u;
+            const uint32_t m = half_ballot(freev);
+            const int before = __popc(m & ((1u << hl) - 1u));
+            if (vv) pos[v] = freev ? nf + before : -1;
+            if (freev && nf + before < NF) fid[nf + before] = v;
+            nf += __popc(m);
+        }
+        if (infeas) status = ST_INFEASIBLE;
+        if (nf > NF) status = ST_BAD_DIMS;
+    }
+    wave_sync();
+    if (status == ST_OK) {
+        for (int id = hl; id < 2 * nf; id += kHalf) {
+            double lo, hi;
+            pair_bound<NU, MODEL>(a, contact, fid[id < nf ? id : id - nf], lo, hi);
+            st[id] = (id < nf) ? (lo > -kInfty ? 1 : 0) : (hi < kInfty ? 1 : 0);
+        }
+    }
+    if (nf > a.max_free) status = ST_BAD_DIMS;
+    wave_sync();
+
+    // ---- S^W_rr = X_r' W X_r over the support rows (w: 0 = Q, 1 = P), entry o = cj NU + ci
+#pragma unroll
+    for (int blk = 0; blk < 4; ++blk) {
+        const int r_ = blk & 1, w_ = blk >> 1;
+        const int lo = r_ ? Sup::x1lo : Sup::x0lo;
+        const double *Xr = r_ ? X1 : X0;
+        const double *w = w_ ? a.pd : a.qd;
+        for (int e = hl; e < NRM; e += kHalf) {
+            const int ci = e % NU, cj = e / NU;
+            double acc = 0.0;
+#pragma unroll
+            for (int l = 0; l < SD; ++l) acc += Xr[ci * SD + l] * w[lo + l] * Xr[cj * SD + l];
+            S[e * 4 + blk] = acc;
+        }
+    }
+    // ---- u_m(c) = X0[:,c]' W_m e_m, v_m(c) = X1[:,c]' W_m e_m, m = 1..N
+    for (int e = hl; e < N * NU; e += kHalf) {
+        const int c = e % NU, m = 1 + e / NU;
+        const double md = (double)m, hm2 = 0.5 * md * md;
+        auto el = [&](int l) {
+            const double wl = (m < N) ? a.qd[l] : a.pd[l];
+            return wl * (x0g[l] + md * Ax[l] + hm2 * A2x[l] - xr[m * NX + l]);
+        };
+        double su = 0.0, sv = 0.0;
+#pragma unroll
+        for (int l = Sup::x0lo; l < Sup::x0hi; ++l) su += X0[c * SD + l - Sup::x0lo] * el(l);
+#pragma unroll
+        for (int l = Sup::x1lo; l < Sup::x1hi; ++l) sv += X1[c * SD + l - Sup::x1lo] * el(l);
+        UV[(m * 2 + 0) * NU + c] = su;
+        UV[(m * 2 + 1) * NU + c] = sv;
+    }
+    wave_sync();
+
+    // ---- g (lane p: g_p), then H_FF over the dead early view (lane p loads row p)
+    const bool ok = valid && status == ST_OK && nf > 0;
+    double gp = 0.0;
+    if (ok && hl < nf) {
+        const int vi = fid[hl], ki = vi / NU, ci = vi % NU;
+        double s = 0.0;
+        for (int m = ki + 1; m <= N; ++m) {
+            const double beta = (double)(m - 1 - ki) + 0.5;
+            s += UV[(m * 2 + 0) * NU + ci] + beta * UV[(m * 2 + 1) * NU + ci];
+        }
+        gp = 2.0 * s;
+    }
+    wave_sync();
+    double *Hb = D + Lay::oR;
+    if (ok) {
+        // one lane per block pair (ki >= kj); the beta sums once per block
+        constexpr int NPAIR = N * (N + 1) / 2;
+        int ki = 0, kj = hl;
+        while (kj > ki) { kj -= ki + 1; ++ki; }
+        for (int bp = hl; bp < NPAIR; bp += kHalf) {
+            double c, si, sj, sij;
+            beta_sums(ki + 1, N - 1, ki, kj, c, si, sj, sij);
+            const double bi = (double)(N - 1 - ki) + 0.5, bj = (double)(N - 1 - kj) + 0.5;
+            const double bij = bi * bj;
+            int mi = 0, mj = 0;
+#pragma unroll
+            for (int cc = 0; cc < NU; ++cc) {
+                mi |= (pos[ki * NU + cc] >= 0) << cc;
+                mj |= (pos[kj * NU + cc] >= 0) << cc;
+            }
+            for (int ri = mi; ri; ri &= ri - 1) {
+                const int ci = __builtin_ctz(ri), pp = pos[ki * NU + ci];
+                for (int rj = mj; rj; rj &= rj - 1) {
+                    const int cj = __builtin_ctz(rj), qq = pos[kj * NU + cj];
+                    if (pp >= qq) {
+                        const double *So = S + (cj * NU + ci) * 4;
+                        double v = c * So[0] + sij * So[1];
+                        v += So[2] + bij * So[3];
+                        if (ki == kj) v += Rm[cj * NU + ci];
+                        Hb[lrow(pp) + qq] = 2.0 * v;
+                    }
+                }
+            }
+            kj += kHalf;
+            while (kj > ki) { kj -= ki + 1; ++ki; }
+        }
+    }
+    wave_sync();
+    double h[NF];
+#pragma unroll
+    for (int q = 0; q < NF; ++q) {
+        const bool in = ok && hl < nf && q < nf && q <= hl;
+        h[q] = in ? Hb[lrow(hl) + q] : ((q == hl) ? 1.0 : 0.0);
+    }
+    wave_sync();
+
+    // ---- solver (gi_run_reg with NF = 31 per half)
+    double *Lc = D + Lay::oR, *R = D + Lay::oR;
+    double *rowbuf = D + Lay::oRow, *colb = rowbuf + NP, *rot = rowbuf + 2 * NP,
+           *rinv = rowbuf + 4 * NP;
+    double fval = 0.0, x = 0.0, u = 0.0;
+    int iters = 0, q = 0, act = -1;
+    double Jr[NF];
+    double gv = gp;
+    const bool any_ok = __ballot(ok) != 0ull;
+    bool ok2 = ok;
+    if (any_ok) {
+        // ---- Cholesky, right-looking, lane l owns row l (identity padding beyond nf)
+        double piv = hread(h[0], 0);
+        bool bad = !(piv > 0.0);
+        double ik = rsqrt_nr(piv);
+#pragma unroll
+        for (int k = 0; k < NF; ++k) {
+            const double lik = h[k] * ik;
+            h[k] = lik;
+            if (hl >= k && hl < NF) Lc[ccol(k, NF) + hl - k] = lik;
+            if (hl == 0) rowbuf[k] = ik;
+            double pivn = 1.0, ikn = 1.0;
+            if (k + 1 < NF) {
+                pivn = hread(h[k + 1 < NF ? k + 1 : k] - lik * lik, k + 1);
+                bad |= !(pivn > 0.0);
+                ikn = rsqrt_nr(pivn);
+            }
+            wave_sync();
+#pragma unroll
+            for (int j = 0; j < NF; ++j) {
+                if (j > k) h[j] -= lik * Lc[ccol(k, NF) + j - k];
+                if ((j & 7) == 7 && j > k) step_fence();
+            }
+#pragma unroll
+            for (int j = 0; j < NF; ++j)
+                if (j >= k) pin(h[j]);
+            piv = pivn;
+            ik = ikn;
+            pin(piv);
+            pin(ik);
+            step_fence();
+        }
+        if (ok && bad) status = ST_NOT_PD;
+        ok2 = ok && status == ST_OK;
+        // ---- columns of L^-1 (rows of J) in registers; lane 31 of each half solves L t = g
+        if (hl < NF) colb[hl] = gv;
+        wave_sync();
+#pragma unroll
+        for (int l = 0; l < NF; ++l) {
+            Jr[l] = (hl == l) ? 1.0 : 0.0;
+            Jr[l] = (hl == kHalf - 1) ? colb[l] : Jr[l];
+        }
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            Jr[i] *= rowbuf[i];
+#pragma unroll
+            for (int l = 0; l < NF; ++l) {
+                if (l > i) Jr[l] -= Lc[ccol(i, NF) + l - i] * Jr[i];
+                if ((l & 15) == 15 && l > i) step_fence();
+            }
+#pragma unroll
+            for (int l = 0; l < NF; ++l)
+                if (l >= i) pin(Jr[l]);
+            step_fence();
+        }
+        // ---- unconstrained minimum x = -J t, objective -|t|^2 / 2
+        wave_sync();
+        if (hl == kHalf - 1) {
+#pragma unroll
+            for (int j = 0; j < NF; ++j) colb[j] = Jr[j];
+        }
+        wave_sync();
+        gv = (hl < NF) ? colb[hl] : 0.0;
+        double s4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int j = 0; j < NF; ++j) {
+            s4[j & 3] += Jr[j] * colb[j];
+            if ((j & 7) == 7) step_fence();
+        }
+        x = (ok2 && hl < nf) ? -((s4[0] + s4[1]) + (s4[2] + s4[3])) : 0.0;
+        fval = half_sum(hl < nf ? gv * gv : 0.0);
+        fval = ok2 ? -0.5 * fval : 0.0;
+        if (ok2 && hl < nf) xs[hl] = x;
+        wave_sync();
+    }
+
+    // ---- dual active-set loop, flattened (one add or drop per pass); the wave runs while
+    //      either half has work
+    const int mt = 2 * nf;
+    const int max_iter = a.max_iter > 0 ? a.max_iter : 10 * (mt + nf + 1);
+    bool done = !ok2;
+    bool fresh = true;
+    int p = 0;
+    while (__ballot(!done) != 0ull) {
+        double dj = 0.0, sp = 0.0, z = 0.0, zn = 0.0, r = 0.0, t1 = INFINITY, t2 = INFINITY;
+        double t = 0.0;
+        int kslot = 0x7fffffff;
+        if (!done && fresh) {
+            // ---- most violated inactive bound (lowest id on ties)
+            double best = INFINITY;
+            int bid = 0x7fffffff;
+            for (int id = hl; id < mt; id += kHalf) {
+                if (st[id] != 1) continue;
+                const bool lower = id < nf;
+                const int a_ = lower ? id : id - nf;
+                const double bb = pair_free_b<NU, MODEL>(a, fid[a_], !lower);
+                const double sl_ = (lower ? xs[a_] : -xs[a_]) - bb;
+                if (sl_ < -kFeasTol * (1.0 + fabs(bb)) && sl_ < best) { best = sl_; bid = id; }
+            }
+            half_argmin(best, bid);
+            if (bid == 0x7fffffff) {
+                done = true;  // optimal
+            } else {
+                p = bid;
+                if (hl == q) u = 0.0;
+                fresh = false;
+            }
+        }
+        if (!done) {
+            // ---- d = J' n_p (lane a's J row through LDS) and the slack of p
+            const bool lower = p < nf;
+            const int a_ = lower ? p : p - nf;
+            const double sg = lower ? 1.0 : -1.0;
+            const double bp = pair_free_b<NU, MODEL>(a, fid[a_], !lower);
+            if (hl == a_) {
+#pragma unroll
+                for (int c = 0; c < NF; ++c) rowbuf[c] = Jr[c];
+            }
+            wave_sync();
+            dj = (hl < nf) ? sg * rowbuf[hl] : 0.0;
+            sp = sg * xs[a_] - bp;
+            wave_sync();
+            if (iters >= max_iter) { status = ST_ITER_LIMIT; done = true; }
+        }
+        const bool stepping = !done;
+        if (stepping) {
+            ++iters;
+            double dd = hl < nf ? dj * dj : 0.0;
+            zn = (hl >= q && hl < nf) ? dj * dj : 0.0;
+            half_sum2(dd, zn);
+            colb[hl] = (hl >= q) ? dj : 0.0;
+            wave_sync();
+            double z4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int j = 0; j < NF; ++j) {
+                z4[j & 3] += Jr[j] * colb[j];
+                if ((j & 7) == 7) step_fence();
+            }
+            z = (z4[0] + z4[1]) + (z4[2] + z4[3]);
+            // r = R^-1 d(0:q): uniform loop to the larger q of the two halves
+            const int qmax = max(__builtin_amdgcn_readlane(q, 0), __builtin_amdgcn_readlane(q, kHalf));
+            if (q > 0) {
+                double val = dj;
+                for (int j = qmax - 1; j >= 0; --j) {
+                    const double rj = hread(val, j) * rinv[j];
+                    if (j < q) {
+                        if (hl == j) r = rj;
+                        if (hl < j) val -= R[roff(j) + hl] * rj;
+                    }
+                }
+                const double rmax = half_max(hl < q ? fabs(r) : 0.0);
+                if (hl < q && r > kRTol * rmax) { t1 = u / r; kslot = hl; }
+                half_argmin(t1, kslot);
+            }
+            const bool dep = !(zn > kDepTol * dd);
+            t2 = dep ? INFINITY : -sp / zn;
+            t = t1 < t2 ? t1 : t2;
+            if (isinf(t)) { status = ST_INFEASIBLE; done = true; }
+        }
+        const bool moving = stepping && !done;
+        bool add = false;
+        if (moving) {
+            const double uq = hread_k(u, q);
+            if (!isinf(t2)) {
+                if (hl < nf) { x += t * z; xs[hl] = x; }
+                fval += t * zn * (0.5 * t + uq);
+            }
+            if (hl < q) u -= t * r;
+            if (hl == q) u += t;
+            add = !isinf(t2) && t2 <= t1;
+            if (add) {
+                // ---- add p: the Givens chain's rotations from suffix sums of d^2
+                const double t0 = half_suffix_sum(hl < nf ? dj * dj : 0.0);
+                if (hl < NF) { colb[hl] = t0; rot[hl] = dj; }
+                wave_sync();
+                const double tm1 = (hl >= 1 && hl <= NF) ? colb[hl - 1] : t0;
+                const double dm1 = (hl >= 1 && hl <= NF) ? rot[hl - 1] : 0.0;
+                const double tp1 = (hl + 1 < NF) ? colb[hl + 1] : 0.0;
+                wave_sync();
+                const double accl = (tp1 == 0.0) ? dj : sqrt(t0);
+                double cl = 1.0, sl = 0.0;
+                if (hl > q && hl < nf && accl != 0.0) {
+                    const double ih = rsqrt_nr(tm1);
+                    cl = dm1 * ih;
+                    sl = accl * ih;
+                }
+                if (hl < NF) { rot[2 * hl] = cl; rot[2 * hl + 1] = sl; }
+                const double rqq = hread_k(accl, q);
+                if (hl < q) R[roff(q) + hl] = dj;
+                if (hl == q) { R[roff(q) + q] = rqq; rinv[q] = 1.0 / rqq; act = p; }
+                if (hl == 0) st[p] = 2;
+                ++q;
+                fresh = true;
+            } else {
+                // ---- drop slot kslot: shift u / act and R's columns left, then Givens back
+                //      to triangular; the (c, s) pairs go to LDS for J
+                const int k = kslot;
+                const int dropped = hread_k(act, k);
+                if (hl == 0) st[dropped] = 1;
+                {
+                    const int src = (hl + 1 < kHalf) ? ln + 1 : ln;
+                    const double un = __shfl(u, src, kWave);
+                    const int an = __shfl(act, src, kWave);
+                    if (hl >= k && hl < q) { u = un; act = an; }
+                }
+                for (int j = k; j < q - 1; ++j) {
+                    const double v = (hl <= j + 1) ? R[roff(j + 1) + hl] : 0.0;
+                    wave_sync();
+                    if (hl <= j + 1) R[roff(j) + hl] = v;
+                    wave_sync();
+                }
+                --q;
+                rot[2 * hl] = 1.0;
+                rot[2 * hl + 1] = 0.0;
+                wave_sync();
+                for (int j = k; j < q; ++j) {
+                    const double aa = R[roff(j) + j], bb = R[roff(j) + j + 1];
+                    if (bb != 0.0) {
+                        const double hh = sqrt(aa * aa + bb * bb);
+                        const double ih = 1.0 / hh;
+                        const double c = aa * ih, s_ = bb * ih;
+                        const int l = j + 1 + hl;
+                        double r0 = 0.0, r1 = 0.0;
+                        if (l < q) { r0 = R[roff(l) + j]; r1 = R[roff(l) + j + 1]; }
+                        wave_sync();
+                        if (l < q) {
+                            R[roff(l) + j] = c * r0 + s_ * r1;
+                            R[roff(l) + j + 1] = -s_ * r0 + c * r1;
+                        }
+                        if (hl == 0) {
+                            R[roff(j) + j] = hh;
+                            R[roff(j) + j + 1] = 0.0;
+                            rinv[j] = ih;
+                            rot[2 * j] = c;
+                            rot[2 * j + 1] = s_;
+                        }
+                        wave_sync();
+                    } else {
+                        if (hl == 0) rinv[j] = 1.0 / aa;
+                        wave_sync();
+                    }
+                }
+            }
+        }
+        wave_sync();
+        // ---- the pass's rotations of J (add: pairs (j-1, j) bottom up; drop: (j, j+1))
+        if (moving && add) {
+#pragma unroll
+            for (int j = NF - 1; j >= 1; --j) {
+                const double c = rot[2 * j], s_ = rot[2 * j + 1];
+                const double y0 = Jr[j - 1], y1 = Jr[j];
+                Jr[j - 1] = c * y0 + s_ * y1;
+                Jr[j] = -s_ * y0 + c * y1;
+                if ((j & 7) == 0) step_fence();
+            }
+        }
+        if (moving && !add) {
+#pragma unroll
+            for (int j = 0; j < NF - 1; ++j) {
+                const double c = rot[2 * j], s_ = rot[2 * j + 1];
+                const double y0 = Jr[j], y1 = Jr[j + 1];
+                Jr[j] = c * y0 + s_ * y1;
+                Jr[j + 1] = -s_ * y0 + c * y1;
+                if ((j & 7) == 7) step_fence();
+            }
+        }
+        wave_sync();
+    }
+
+    // ---- outputs
+    if (valid) {
+        double *U = a.U + (size_t)b * NV;
+        const bool have_map = nf <= NF;
+        for (int v = hl; v < NV; v += kHalf) {
+            const int pv = pos[v];
+            if (pv < 0 || !have_map) {
+                double lo, hi;
+                pair_bound<NU, MODEL>(a, contact, v, lo, hi);
+                U[v] = (pv < 0) ? lo : 0.0;
+            }
+        }
+        if (have_map && hl < nf) U[fid[hl]] = x;
+        if (hl == 0) {
+            a.cost[b] = fval;
+            a.status[b] = status;
+            a.iters[b] = iters;
+        }
+    }
+    (void)NS;
+}
+
+}  // namespace mpcqp

@@ -28,6 +28,7 @@
 #include "condense.hpp"
 #include "fused.hpp"
 #include "mpc_fused.hpp"
+#include "mpc_pair.hpp"
 #include "gi_solver.hpp"
 
 using namespace mpcqp;
@@ -373,8 +374,17 @@ __global__ void __launch_bounds__(64, (NF <= 32 ? 3 : 2)) k_mpc_gen(MpcArgs a) {
     fast_mpc<NU, N, MODEL, FRIC, NF, true>(a, smem_g);
 }
 
+// two instances per wavefront (mpc_pair.hpp) for at most 31 free variables: grid = ceil(B/2)
+template <int NU, int N, int MODEL, bool GEN>
+__global__ void __launch_bounds__(64, 3) k_mpc_pair(MpcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_p[];
+    pair_mpc<NU, N, MODEL, GEN>(a, smem_p);
+}
+
 struct FastKernels {
     const void *mpc_gen = nullptr;
+    const void *pair = nullptr, *pair_gen = nullptr;  // two QPs per wave (nf <= 31)
+    size_t pair_lds = 0;
     const void *disc = nullptr, *cs = nullptr, *mpc = nullptr;
     size_t disc_lds = 0, cs_lds = 0, mpc_lds = 0;
     int nx = 0, nu = 0;
@@ -395,19 +405,40 @@ FastKernels make_fast() {
     return k;
 }
 
+template <int NU, int N, int MODEL>
+void add_pair(FastKernels &k) {
+    k.pair = (const void *)&k_mpc_pair<NU, N, MODEL, false>;
+    if constexpr (MODEL == 0) k.pair_gen = (const void *)&k_mpc_pair<NU, N, MODEL, true>;
+    k.pair_lds = PairLayout<NU, N, MODEL>::lds_bytes;
+}
+
+// MPCQP_PAIR=0 in the environment keeps the one-QP-per-wave kernel (A/B measurements)
+bool pair_enabled() {
+    const char *e = getenv("MPCQP_PAIR");
+    return !(e && e[0] == '0');
+}
+
 // instantiated configurations (BASELINE configs A/B/C and the literal model); anything else
 // runs the generic runtime-dimension kernels
 bool pick_fast(int model, int nx, int nu, int N, bool fric, int nfmax, FastKernels &k) {
     if (nx != 13) return false;
     if (model == MPCQP_MODEL_SRBM && nu == 6) {
-        if (N == 10 && nfmax <= 32) { k = fric ? make_fast<13, 6, 10, 0, true, 32>() : make_fast<13, 6, 10, 0, false, 32>(); return true; }
+        if (N == 10 && nfmax <= 32) {
+            k = fric ? make_fast<13, 6, 10, 0, true, 32>() : make_fast<13, 6, 10, 0, false, 32>();
+            if (!fric && nfmax <= kPairNF && pair_enabled()) add_pair<6, 10, 0>(k);
+            return true;
+        }
         if (N == 10 && nfmax <= 64) { k = fric ? make_fast<13, 6, 10, 0, true, 64>() : make_fast<13, 6, 10, 0, false, 64>(); return true; }
         if (N == 20 && nfmax <= 64) { k = fric ? make_fast<13, 6, 20, 0, true, 64>() : make_fast<13, 6, 20, 0, false, 64>(); return true; }
         return false;
     }
     if (model == MPCQP_MODEL_LITERAL && nu == 3 && !fric) {
         if (N == 20 && nfmax <= 64) { k = make_fast<13, 3, 20, 1, false, 64>(); return true; }
-        if (N == 10 && nfmax <= 32) { k = make_fast<13, 3, 10, 1, false, 32>(); return true; }
+        if (N == 10 && nfmax <= 32) {
+            k = make_fast<13, 3, 10, 1, false, 32>();
+            if (nfmax <= kPairNF && pair_enabled()) add_pair<3, 10, 1>(k);
+            return true;
+        }
     }
     return false;
 }
@@ -934,6 +965,13 @@ static int launch(const void *k, int B, size_t lds, hipStream_t s, void *arg) {
     return hip_status(hipLaunchKernel(k, dim3(B), dim3(64), args, lds, s));
 }
 
+// the fused step: two instances per wave when the paired kernel is instantiated
+static int launch_mpc(mpcqp_ctx *c, bool gen, int B, MpcArgs *a) {
+    const void *pk = gen ? c->fk.pair_gen : c->fk.pair;
+    if (pk) return launch(pk, (B + 1) / 2, c->fk.pair_lds, c->stream, a);
+    return launch(gen ? c->fk.mpc_gen : c->fk.mpc, B, c->fk.mpc_lds, c->stream, a);
+}
+
 int mpcqp_batch_condense(mpcqp_ctx *c, int B, const double *x0, const double *xref,
                          const double *lin, double *H, double *f) {
     if (!c || !x0 || !xref || !lin || !H || !f || B < 0) return MPCQP_ERR_BAD_ARG;
@@ -1089,7 +1127,7 @@ int mpcqp_batch_solve(mpcqp_ctx *c, int B, const double *x0, const double *xref,
         a.status = status;
         a.iters = iters;
         tbegin(c, 1);
-        const int rc = launch(c->fk.mpc, B, c->fk.mpc_lds, c->stream, &a);
+        const int rc = launch_mpc(c, false, B, &a);
         tend(c, 1);
         return rc;
     }
@@ -1171,7 +1209,7 @@ int mpcqp_batch_solve_gait(mpcqp_ctx *c, int S, int C, const double *state, cons
     a.status = status;
     a.iters = iters;
     tbegin(c, 1);
-    const int rc = launch(c->fk.mpc_gen, B, c->fk.mpc_lds, c->stream, &a);
+    const int rc = launch_mpc(c, true, B, &a);
     tend(c, 1);
     return rc;
 }

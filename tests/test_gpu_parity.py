@@ -273,3 +273,61 @@ def test_generic_path_non_diagonal_weights(gpu, orc):
     assert np.all(o["status"] == 0)
     for i in range(128):
         assert u_close(o["U"][i], ref["U"][i]), i
+
+
+def test_pair_kernel_matches_single_and_oracle(gpu, orc, monkeypatch):
+    """Two QPs per wavefront (csrc/mpc_pair.hpp, nf <= 31) against the one-QP-per-wave kernel
+    (MPCQP_PAIR=0) and the oracle: odd batch (the last wave's upper half is idle), contact
+    masks with fewer stance forces (nf < 30, uneven iteration counts inside a wave) and with
+    both feet down at one step (nf > max_free -> BAD_DIMS beside a solved neighbour)."""
+    import mpcqp
+    p = mpcqp.model_params("B")
+    B = 333
+    batch = mpcqp.make_batch(p, B, seed=7)
+    ct = batch["contact"].astype(np.uint64).copy()
+    rng = np.random.default_rng(11)
+    for i in range(B):
+        if i % 5 == 1:  # lift the stance foot for a few random steps
+            for k in rng.choice(p["N"], 3, replace=False):
+                ct[i] &= ~np.uint64(3 << (2 * int(k)))
+        if i % 7 == 3:  # double support at one step: 33 free forces
+            ct[i] |= np.uint64(3 << (2 * int(rng.integers(p["N"]))))
+    batch["contact"] = ct
+    monkeypatch.setenv("MPCQP_PAIR", "0")
+    single = run_batch(p, batch)
+    monkeypatch.delenv("MPCQP_PAIR")
+    pair = run_batch(p, batch)
+    nfree = np.array([3 * bin(int(c)).count("1") for c in ct])
+    bad_dims = nfree > p["max_free"]
+    assert bad_dims.sum() > 20 and (nfree < 30).sum() > 20
+    np.testing.assert_array_equal(pair["status"], single["status"])
+    assert np.all(pair["status"][bad_dims] == 1) and np.all(pair["status"][~bad_dims] == 0)
+    np.testing.assert_array_equal(pair["iters"], single["iters"])
+    np.testing.assert_allclose(pair["U"], single["U"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(pair["cost"], single["cost"], rtol=1e-12, atol=1e-12)
+    ok = ~bad_dims
+    ref = orc.srbm_batch(p, batch["x0"][ok], batch["xref"][ok], batch["lin"][ok], ct[ok])
+    assert np.all(ref["status"] == 0)
+    Uo = pair["U"][ok]
+    bad = [j for j in range(Uo.shape[0]) if not u_close(Uo[j], ref["U"][j])]
+    assert not bad, bad[:10]
+    np.testing.assert_allclose(pair["cost"][ok], ref["cost"], rtol=1e-9, atol=1e-9)
+    assert len(set(pair["iters"][ok].tolist())) > 2  # uneven work inside the waves
+
+
+def test_pair_kernel_literal_model(gpu, orc, monkeypatch):
+    """reference-literal 13/3/10 (nf = 30) through the paired kernel vs the one-QP kernel"""
+    import mpcqp
+    p = mpcqp.model_params("L", N=10)
+    B = 257
+    batch = mpcqp.make_batch(p, B, seed=3)
+    monkeypatch.setenv("MPCQP_PAIR", "0")
+    single = run_batch(p, batch)
+    monkeypatch.delenv("MPCQP_PAIR")
+    pair = run_batch(p, batch)
+    np.testing.assert_array_equal(pair["status"], single["status"])
+    np.testing.assert_array_equal(pair["iters"], single["iters"])
+    np.testing.assert_allclose(pair["U"], single["U"], rtol=0, atol=1e-12)
+    ref = orc.srbm_batch(p, batch["x0"], batch["xref"], batch["lin"], batch["contact"])
+    for i in range(B):
+        assert u_close(pair["U"][i], ref["U"][i]), i
