@@ -1,0 +1,86 @@
+// fast_kernels.hpp -- the compile-time-dimension kernels of the fused hot path and their
+// per-configuration instantiation.  Each configuration family is instantiated in its own
+// translation unit (fast_srbm10.hip, fast_srbm20.hip, fast_literal.hip, fast_pair.hip) so the
+// library builds in parallel; mpcqp_kernels.hip picks one through pick_fast().
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/mpcqp.h"
+
+#ifndef MPCQP_W32
+#define MPCQP_W32 3  // waves per SIMD the NF <= 32 fused kernel is register-budgeted for
+#endif
+#include "condense.hpp"
+#include "fused.hpp"
+#include "mpc_fused.hpp"
+
+namespace mpcqp {
+
+struct FastKernels {
+    const void *mpc_gen = nullptr;
+    const void *pair = nullptr, *pair_gen = nullptr;  // two QPs per wave (nf <= 31)
+    size_t pair_lds = 0;
+    const void *disc = nullptr, *cs = nullptr, *mpc = nullptr;
+    size_t disc_lds = 0, cs_lds = 0, mpc_lds = 0;
+    int nx = 0, nu = 0;
+};
+
+// per-family pickers (one translation unit each); false = not instantiated
+bool pick_fast_srbm10(bool fric, int nfmax, FastKernels &k);
+bool pick_fast_srbm20(bool fric, int nfmax, FastKernels &k);
+bool pick_fast_literal(int N, int nfmax, FastKernels &k);
+// two-QPs-per-wave kernels (fast_pair.hip), added to k for nf <= 31 configurations
+bool add_fast_pair(int model, int N, bool fric, int nfmax, FastKernels &k);
+
+#ifdef MPCQP_FAST_TU
+namespace {
+
+template <int NX, int NU, int MODEL>
+__global__ void __launch_bounds__(64) k_discretize(FastArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double smem_f[];
+    if ((int)blockIdx.x >= a.B) return;
+    fast_discretize<NX, NU, MODEL>(a, smem_f);
+}
+
+template <int NX, int NU, int N, int MODEL, bool FRIC, int NFMAX>
+__global__ void __launch_bounds__(64) k_condense_solve(FastArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_c[];
+    if ((int)blockIdx.x >= a.B) return;
+    fast_condense_solve<NX, NU, N, MODEL, FRIC, NFMAX>(a, smem_c);
+}
+
+template <int NU, int N, int MODEL, bool FRIC, int NF>
+__global__ void __launch_bounds__(64, (NF <= 32 ? MPCQP_W32 : 2)) k_mpc(MpcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_m[];
+    if ((int)blockIdx.x >= a.B) return;
+    fast_mpc<NU, N, MODEL, FRIC, NF>(a, smem_m);
+}
+
+// device-generated inputs: the same fused step, x0/xref/lin/contact
+// built on chip from per-state data, gait candidates and commands
+template <int NU, int N, int MODEL, bool FRIC, int NF>
+__global__ void __launch_bounds__(64, (NF <= 32 ? 3 : 2)) k_mpc_gen(MpcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_g[];
+    if ((int)blockIdx.x >= a.B) return;
+    fast_mpc<NU, N, MODEL, FRIC, NF, true>(a, smem_g);
+}
+
+}  // namespace
+
+template <int NX, int NU, int N, int MODEL, bool FRIC, int NFMAX>
+FastKernels make_fast() {
+    FastKernels k;
+    k.disc = (const void *)&k_discretize<NX, NU, MODEL>;
+    k.cs = (const void *)&k_condense_solve<NX, NU, N, MODEL, FRIC, NFMAX>;
+    k.disc_lds = sizeof(double) * disc_lds_doubles<NX, NU>();
+    k.cs_lds = CSLayout<NX, NU, N, FRIC, NFMAX>::lds_bytes;
+    k.mpc = (const void *)&k_mpc<NU, N, MODEL, FRIC, NFMAX>;
+    if constexpr (MODEL == 0) k.mpc_gen = (const void *)&k_mpc_gen<NU, N, MODEL, FRIC, NFMAX>;
+    k.mpc_lds = MpcLayout<NU, N, FRIC, NFMAX>::lds_bytes;
+    k.nx = NX;
+    k.nu = NU;
+    return k;
+}
+#endif  // MPCQP_FAST_TU
+
+}  // namespace mpcqp

@@ -1,0 +1,14 @@
+// fast_literal.hip -- the reference-literal 13/3 model (include/mpcQP.h:154-181) at N = 20
+// and N = 10 (fast_pair.hip adds the paired kernel for nf <= 31).
+#define MPCQP_FAST_TU
+#include "fast_kernels.hpp"
+
+namespace mpcqp {
+
+bool pick_fast_literal(int N, int nfmax, FastKernels &k) {
+    if (N == 20 && nfmax <= 64) { k = make_fast<13, 3, 20, 1, false, 64>(); return true; }
+    if (N == 10 && nfmax <= 32) { k = make_fast<13, 3, 10, 1, false, 32>(); return true; }
+    return false;
+}
+
+}  // namespace mpcqp

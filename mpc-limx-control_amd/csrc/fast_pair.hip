@@ -1,0 +1,36 @@
+// fast_pair.hip -- the two-QPs-per-wavefront fused kernels (mpc_pair.hpp) for configurations
+// with at most 31 free variables: SRBM 13/6/10 box (config B, explicit and generated inputs)
+// and the reference-literal 13/3/10.
+#include <hip/hip_runtime.h>
+
+#include "../../include/mpcqp.h"
+#include "fast_kernels.hpp"
+#include "mpc_pair.hpp"
+
+namespace mpcqp {
+namespace {
+
+// grid = ceil(B / 2): lanes 0-31 solve instance 2w, lanes 32-63 instance 2w + 1
+template <int NU, int N, int MODEL, bool GEN>
+__global__ void __launch_bounds__(64, 3) k_mpc_pair(MpcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_p[];
+    pair_mpc<NU, N, MODEL, GEN>(a, smem_p);
+}
+
+template <int NU, int N, int MODEL>
+void add_pair(FastKernels &k) {
+    k.pair = (const void *)&k_mpc_pair<NU, N, MODEL, false>;
+    if constexpr (MODEL == 0) k.pair_gen = (const void *)&k_mpc_pair<NU, N, MODEL, true>;
+    k.pair_lds = PairLayout<NU, N, MODEL>::lds_bytes;
+}
+
+}  // namespace
+
+bool add_fast_pair(int model, int N, bool fric, int nfmax, FastKernels &k) {
+    if (fric || N != 10 || nfmax > kPairNF) return false;
+    if (model == MPCQP_MODEL_SRBM && k.nu == 6) { add_pair<6, 10, 0>(k); return true; }
+    if (model == MPCQP_MODEL_LITERAL && k.nu == 3) { add_pair<3, 10, 1>(k); return true; }
+    return false;
+}
+
+}  // namespace mpcqp

@@ -9,6 +9,9 @@
 //   k_solve      corrected dense QP, Goldfarb-Idnani                  src/QPSolver.cpp:83-106
 //   k_discretize<..>, k_condense_solve<..>   the batched hot path with compile-time dims
 //                (fused.hpp): linearise + expm, then Phi, H_FF, f and the solve in LDS
+//   k_mpc<..>, k_mpc_gen<..>   the whole tick in one kernel (mpc_fused.hpp), one QP per wave
+//   k_mpc_pair<..>             the same, two QPs per wave for nf <= 31 (mpc_pair.hpp)
+//                (instantiated in fast_srbm10 / fast_srbm20 / fast_literal / fast_pair.hip)
 //   k_select_min per-rank min-cost key (multi-GPU selection)
 //   k_plant      x <- Ad x + Bd u                                       src/QPSolver.cpp:108-111
 #include <hip/hip_runtime.h>
@@ -22,13 +25,7 @@
 
 #include "../../include/mpcqp.h"
 
-#ifndef MPCQP_W32
-#define MPCQP_W32 3  // waves per SIMD the NF <= 32 fused kernel is register-budgeted for
-#endif
-#include "condense.hpp"
-#include "fused.hpp"
-#include "mpc_fused.hpp"
-#include "mpc_pair.hpp"
+#include "fast_kernels.hpp"
 #include "gi_solver.hpp"
 
 using namespace mpcqp;
@@ -343,75 +340,6 @@ __global__ void __launch_bounds__(64) k_plant_srbm(PlantArgs a) {
     for (int c = ln; c < a.C; c += 64) a.phase[(size_t)s * a.C + c] += a.Ts;
 }
 
-// ------------------------------------------------------------------ fast path kernels
-template <int NX, int NU, int MODEL>
-__global__ void __launch_bounds__(64) k_discretize(FastArgs a) {
-    extern __shared__ __attribute__((aligned(16))) double smem_f[];
-    if ((int)blockIdx.x >= a.B) return;
-    fast_discretize<NX, NU, MODEL>(a, smem_f);
-}
-
-template <int NX, int NU, int N, int MODEL, bool FRIC, int NFMAX>
-__global__ void __launch_bounds__(64) k_condense_solve(FastArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_c[];
-    if ((int)blockIdx.x >= a.B) return;
-    fast_condense_solve<NX, NU, N, MODEL, FRIC, NFMAX>(a, smem_c);
-}
-
-template <int NU, int N, int MODEL, bool FRIC, int NF>
-__global__ void __launch_bounds__(64, (NF <= 32 ? MPCQP_W32 : 2)) k_mpc(MpcArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_m[];
-    if ((int)blockIdx.x >= a.B) return;
-    fast_mpc<NU, N, MODEL, FRIC, NF>(a, smem_m);
-}
-
-// device-generated inputs: the same fused step, x0/xref/lin/contact
-// built on chip from per-state data, gait candidates and commands
-template <int NU, int N, int MODEL, bool FRIC, int NF>
-__global__ void __launch_bounds__(64, (NF <= 32 ? 3 : 2)) k_mpc_gen(MpcArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_g[];
-    if ((int)blockIdx.x >= a.B) return;
-    fast_mpc<NU, N, MODEL, FRIC, NF, true>(a, smem_g);
-}
-
-// two instances per wavefront (mpc_pair.hpp) for at most 31 free variables: grid = ceil(B/2)
-template <int NU, int N, int MODEL, bool GEN>
-__global__ void __launch_bounds__(64, 3) k_mpc_pair(MpcArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem_p[];
-    pair_mpc<NU, N, MODEL, GEN>(a, smem_p);
-}
-
-struct FastKernels {
-    const void *mpc_gen = nullptr;
-    const void *pair = nullptr, *pair_gen = nullptr;  // two QPs per wave (nf <= 31)
-    size_t pair_lds = 0;
-    const void *disc = nullptr, *cs = nullptr, *mpc = nullptr;
-    size_t disc_lds = 0, cs_lds = 0, mpc_lds = 0;
-    int nx = 0, nu = 0;
-};
-
-template <int NX, int NU, int N, int MODEL, bool FRIC, int NFMAX>
-FastKernels make_fast() {
-    FastKernels k;
-    k.disc = (const void *)&k_discretize<NX, NU, MODEL>;
-    k.cs = (const void *)&k_condense_solve<NX, NU, N, MODEL, FRIC, NFMAX>;
-    k.disc_lds = sizeof(double) * disc_lds_doubles<NX, NU>();
-    k.cs_lds = CSLayout<NX, NU, N, FRIC, NFMAX>::lds_bytes;
-    k.mpc = (const void *)&k_mpc<NU, N, MODEL, FRIC, NFMAX>;
-    if constexpr (MODEL == 0) k.mpc_gen = (const void *)&k_mpc_gen<NU, N, MODEL, FRIC, NFMAX>;
-    k.mpc_lds = MpcLayout<NU, N, FRIC, NFMAX>::lds_bytes;
-    k.nx = NX;
-    k.nu = NU;
-    return k;
-}
-
-template <int NU, int N, int MODEL>
-void add_pair(FastKernels &k) {
-    k.pair = (const void *)&k_mpc_pair<NU, N, MODEL, false>;
-    if constexpr (MODEL == 0) k.pair_gen = (const void *)&k_mpc_pair<NU, N, MODEL, true>;
-    k.pair_lds = PairLayout<NU, N, MODEL>::lds_bytes;
-}
-
 // MPCQP_PAIR=0 in the environment keeps the one-QP-per-wave kernel (A/B measurements)
 bool pair_enabled() {
     const char *e = getenv("MPCQP_PAIR");
@@ -422,25 +350,14 @@ bool pair_enabled() {
 // runs the generic runtime-dimension kernels
 bool pick_fast(int model, int nx, int nu, int N, bool fric, int nfmax, FastKernels &k) {
     if (nx != 13) return false;
+    bool found = false;
     if (model == MPCQP_MODEL_SRBM && nu == 6) {
-        if (N == 10 && nfmax <= 32) {
-            k = fric ? make_fast<13, 6, 10, 0, true, 32>() : make_fast<13, 6, 10, 0, false, 32>();
-            if (!fric && nfmax <= kPairNF && pair_enabled()) add_pair<6, 10, 0>(k);
-            return true;
-        }
-        if (N == 10 && nfmax <= 64) { k = fric ? make_fast<13, 6, 10, 0, true, 64>() : make_fast<13, 6, 10, 0, false, 64>(); return true; }
-        if (N == 20 && nfmax <= 64) { k = fric ? make_fast<13, 6, 20, 0, true, 64>() : make_fast<13, 6, 20, 0, false, 64>(); return true; }
-        return false;
+        if (N == 10) found = pick_fast_srbm10(fric, nfmax, k);
+        if (N == 20) found = pick_fast_srbm20(fric, nfmax, k);
     }
-    if (model == MPCQP_MODEL_LITERAL && nu == 3 && !fric) {
-        if (N == 20 && nfmax <= 64) { k = make_fast<13, 3, 20, 1, false, 64>(); return true; }
-        if (N == 10 && nfmax <= 32) {
-            k = make_fast<13, 3, 10, 1, false, 32>();
-            if (nfmax <= kPairNF && pair_enabled()) add_pair<3, 10, 1>(k);
-            return true;
-        }
-    }
-    return false;
+    if (model == MPCQP_MODEL_LITERAL && nu == 3 && !fric) found = pick_fast_literal(N, nfmax, k);
+    if (found && pair_enabled()) add_fast_pair(model, N, fric, nfmax, k);
+    return found;
 }
 
 // ------------------------------------------------------------------------------ host side
