@@ -4,9 +4,9 @@ metric), batch 65,536 per GPU, 1..8 MI355X (one process per GPU, weak scaling: c
 524,288 = 65,536 x 8).
 
 One step = one pass of the hot path over the whole per-GPU batch, inputs resident in HBM:
-  k_mpc (linearise + discretise + condense + Goldfarb-Idnani solve, fused, one QP per
-  wavefront) -> k_select_min (min-cost key) -> [N>1] RCCL MIN all-reduce of the 8-byte key
-  + broadcast of the winner's U (480 B).
+  k_mpc_pair (linearise + discretise + condense + Goldfarb-Idnani solve, fused, two QPs per
+  wavefront; k_mpc, one QP per wavefront, where nf > 30) -> k_select_min (min-cost key)
+  -> [N>1] RCCL MIN all-reduce of the 8-byte key + broadcast of the winner's U (480 B).
 
 Prints ONE JSON line on rank 0 (driver contract).
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config B|C|L]
@@ -50,7 +50,7 @@ def algorithmic_bytes(nx: int, nu: int, N: int):
 
 
 def pmc_traffic(config: str, batch: int):
-    """HBM bytes per k_mpc launch from the committed rocprofv3 PMC summary
+    """HBM bytes per fused-kernel launch from the committed rocprofv3 PMC summary
     (tools/profile_run.sh + tools/summarize_profile.py), if it matches this workload."""
     try:
         t = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
@@ -97,7 +97,7 @@ def cpu_baseline(p, batch, budget_s=12.0):
 
 
 def host_staged_rate(eng, batch, p, reps=5):
-    """QP/s through mpcqp_batch_solve_host: host arrays in, H2D + k_mpc + D2H, synchronous
+    """QP/s through mpcqp_batch_solve_host: host arrays in, H2D + fused kernel + D2H, synchronous
     (the PCIe-inclusive number; never `value`)."""
     import ctypes as C
 
@@ -234,8 +234,8 @@ def main():
                         nu=p["nu"], config=args.config, parallelism=f"dp{world}",
                         solved_frac=solved, mean_solver_iters=float(iters.mean()),
                         fast_path=eng.fast_path,
-                        kernel_ms=dict(k_mpc=mpc_ms, k_select_min=sel_ms)),
-            roofline=dict(bound="mfma", kernel="k_mpc", achieved=achieved,
+                        kernel_ms={eng.fused_kernel: mpc_ms, "k_select_min": sel_ms}),
+            roofline=dict(bound="mfma", kernel=eng.fused_kernel, achieved=achieved,
                           peak=FP64_PEAK_TFLOPS, unit="TFLOP/s",
                           frac=achieved / FP64_PEAK_TFLOPS, traffic=traffic,
                           traffic_source=(f"profiles/{traffic_tag}_summary.json (rocprofv3 PMC, "

@@ -149,8 +149,10 @@ int mpcqp_ctx_destroy(mpcqp_ctx *ctx);
 int mpcqp_set_stream(mpcqp_ctx *ctx, void *stream);
 int mpcqp_sync(mpcqp_ctx *ctx);
 
-/* 1 when the context runs the compile-time-dimension fused kernels (13/6/{10,20} SRBM,
- * 13/3/{10,20} literal, diagonal Q and P), 0 when it runs the generic kernels */
+/* 0 when the context runs the generic kernels; 1 when it runs the compile-time-dimension
+ * fused kernel, one QP per wavefront (13/6/{10,20} SRBM, 13/3/{10,20} literal, diagonal Q and
+ * P); 2 when it runs the fused kernel with two QPs per wavefront (N = 10, box bounds,
+ * max_free <= 30: config B and the literal 13/3/10) */
 int mpcqp_ctx_fast_path(const mpcqp_ctx *ctx);
 
 /* stage 1: linearise + discretise.  AB [B][nx*(nx+nu)] = [Ad | Bd] column-major */

@@ -18,7 +18,7 @@ namespace mpcqp {
 
 struct FastKernels {
     const void *mpc_gen = nullptr;
-    const void *pair = nullptr, *pair_gen = nullptr;  // two QPs per wave (nf <= 31)
+    const void *pair = nullptr, *pair_gen = nullptr;  // two QPs per wave (nf <= 30)
     size_t pair_lds = 0;
     const void *disc = nullptr, *cs = nullptr, *mpc = nullptr;
     size_t disc_lds = 0, cs_lds = 0, mpc_lds = 0;
@@ -29,7 +29,7 @@ struct FastKernels {
 bool pick_fast_srbm10(bool fric, int nfmax, FastKernels &k);
 bool pick_fast_srbm20(bool fric, int nfmax, FastKernels &k);
 bool pick_fast_literal(int N, int nfmax, FastKernels &k);
-// two-QPs-per-wave kernels (fast_pair.hip), added to k for nf <= 31 configurations
+// two-QPs-per-wave kernels (fast_pair.hip), added to k for nf <= 30 configurations
 bool add_fast_pair(int model, int N, bool fric, int nfmax, FastKernels &k);
 
 #ifdef MPCQP_FAST_TU

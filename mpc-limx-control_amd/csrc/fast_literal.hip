@@ -1,5 +1,5 @@
 // fast_literal.hip -- the reference-literal 13/3 model (include/mpcQP.h:154-181) at N = 20
-// and N = 10 (fast_pair.hip adds the paired kernel for nf <= 31).
+// and N = 10 (fast_pair.hip adds the paired kernel for nf <= 30).
 #define MPCQP_FAST_TU
 #include "fast_kernels.hpp"
 

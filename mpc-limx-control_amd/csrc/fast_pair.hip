@@ -1,5 +1,5 @@
 // fast_pair.hip -- the two-QPs-per-wavefront fused kernels (mpc_pair.hpp) for configurations
-// with at most 31 free variables: SRBM 13/6/10 box (config B, explicit and generated inputs)
+// with at most 30 free variables: SRBM 13/6/10 box (config B, explicit and generated inputs)
 // and the reference-literal 13/3/10.
 #include <hip/hip_runtime.h>
 
@@ -7,12 +7,16 @@
 #include "fast_kernels.hpp"
 #include "mpc_pair.hpp"
 
+#ifndef MPCQP_PAIR_W
+#define MPCQP_PAIR_W 3  // waves per SIMD the paired kernel is register-budgeted for
+#endif
+
 namespace mpcqp {
 namespace {
 
 // grid = ceil(B / 2): lanes 0-31 solve instance 2w, lanes 32-63 instance 2w + 1
 template <int NU, int N, int MODEL, bool GEN>
-__global__ void __launch_bounds__(64, 3) k_mpc_pair(MpcArgs a) {
+__global__ void __launch_bounds__(64, MPCQP_PAIR_W) k_mpc_pair(MpcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_p[];
     pair_mpc<NU, N, MODEL, GEN>(a, smem_p);
 }

@@ -1,6 +1,6 @@
 // fast_srbm10.hip -- SRBM 13/6/10 instantiations (BASELINE config B, the metric; box or
 // friction rows): one-QP-per-wave kernels for NF <= 32 / 64 (fast_pair.hip adds the paired
-// kernel for nf <= 31).
+// kernel for nf <= 30).
 #define MPCQP_FAST_TU
 #include "fast_kernels.hpp"
 

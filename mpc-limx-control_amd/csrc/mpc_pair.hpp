@@ -4,12 +4,12 @@
 // Reference: mpcQP::mpcQP + buildSystemModel (include/mpcQP.h:35-119, 121-182),
 // QPSolver::discretizeSystem / buildQPParams / solveQP (src/QPSolver.cpp:21-106).
 //
-// For problems with at most 31 free variables -- config B (SRBM 13/6/10: the gait has one
+// For problems with at most 30 free variables -- config B (SRBM 13/6/10: the gait has one
 // stance foot per horizon step, nf = 30) and the reference-literal 13/3/10 model (nf = 30) --
 // the one-QP-per-wave kernel leaves lanes 32-63 idle through the factorisation, the inverse
 // and the dual loop, and an FP64 wave instruction costs 4 cycles however many lanes it uses.
 // Here every lane-parallel phase serves two instances for the same instruction count:
-//   * lane l of a half owns row l of H_FF / L and row l of J (31 columns in registers); lane
+//   * lane l of a half owns row l of H_FF / L and row l of J (30 columns in registers); lane
 //     31 of each half carries g through the inverse sweep (t = L^-1 g), as lane 63 does in
 //     gi_reg.hpp
 //   * broadcasts are LDS reads at a per-half address (one address per half); cross-lane reads
@@ -25,25 +25,37 @@
 // over them, and the bounds' b are recomputed from the free map -- so three waves (six QPs)
 // per SIMD fit in 160 KB.
 #pragma once
+#include "half_ops.hpp"
 #include "mpc_fused.hpp"
 
 namespace mpcqp {
 
-constexpr int kPairNF = 31;  // free variables per instance; lane 31 of a half carries g
+// LDS loads in flight per step of the unrolled sweeps (a code-motion fence every PF elements):
+// larger hides more LDS latency behind the FMAs, smaller bounds the registers the loads hold
+#ifndef MPCQP_PF_CHOL
+#define MPCQP_PF_CHOL 8
+#endif
+#ifndef MPCQP_PF_INV
+#define MPCQP_PF_INV 16
+#endif
+#ifndef MPCQP_PF_DUAL
+#define MPCQP_PF_DUAL 8
+#endif
+
+constexpr int kPairNF = 30;  // free variables per instance; lane 31 of a half carries g
 
 template <int NU, int N, int MODEL>
 struct PairLayout {
-    static constexpr int NX = 13, NF = kPairNF, NV = NU * N, MT = 2 * NF, NP = kHalf;
+    static constexpr int NX = 13, NF = kPairNF, NV = NU * N, NP = kHalf;
     using Sup = XSupport<MODEL>;
     static constexpr int SD = Sup::x0hi - Sup::x0lo;
     static constexpr int NR = RegPack<NF>::doubles;  // packed L / R
     static constexpr int HB = NF * (NF + 1) / 2;     // packed H_FF
-    // doubles.  Live for the whole kernel: the x mirror.  Then one region, in turn:
+    // doubles; one region, in turn:
     //   early   : X0, X1 support rows, A x0, A^2 x0, xref, x0, then u_m / v_m   [oU, eUV)
     //   H build : packed H [oU, oU + HB) over the dead early view; S and the R copy after it
     //   solver  : packed L / R [oU, oU + NR), then 5 x 32 broadcast doubles
-    static constexpr int oXS = 0;
-    static constexpr int oU = NP;
+    static constexpr int oU = 0;
     static constexpr int oX0 = oU;                       // [NU][SD]
     static constexpr int oX1 = oX0 + NU * SD;            // [NU][SD]
     static constexpr int oAx = oX1 + NU * SD;            // NX
@@ -58,9 +70,10 @@ struct PairLayout {
     static constexpr int oR = oU;
     static constexpr int oRow = (oR + NR + 1) & ~1;      // buf | colb | rot (2 NP) | 1/R(j,j)
     static constexpr int eLate = oRow + 5 * NP;
-    static constexpr int nDoubles = ((eMid > eLate ? eMid : eLate) + 1) & ~1;
+    static constexpr int oCt = ((eMid > eLate ? eMid : eLate) + 1) & ~1;  // contact mask (u64)
+    static constexpr int nDoubles = oCt + 2;
     static constexpr size_t bytes =
-        (sizeof(double) * nDoubles + sizeof(int) * (NF + NV) + ((MT + 15) & ~15) + 15) & ~(size_t)15;
+        (sizeof(double) * nDoubles + sizeof(int) * (NF + NV) + 15) & ~(size_t)15;
     static constexpr size_t lds_bytes = 2 * bytes;  // both halves
     static_assert(oU % 2 == 0 && oRow % 2 == 0 && oS % 2 == 0, "16-byte aligned buffers");
     static_assert(HB <= NR, "packed H fits the L / R space");
@@ -78,15 +91,6 @@ __device__ __forceinline__ void pair_bound(const MpcArgs &a, uint64_t contact, i
         else { lo = -a.fxy_max; hi = a.fxy_max; }
     } else { lo = 0.0; hi = 0.0; }
 }
-// b of the one-sided bound constraint on FREE variable v (a free SRBM force is in contact):
-// lower x >= lo (b = lo), upper -x >= -hi (b = -hi) -- gi_cons_b without the LDS table
-template <int NU, int MODEL>
-__device__ __forceinline__ double pair_free_b(const MpcArgs &a, int v, bool upper) {
-    if (MODEL == 1) return upper ? -a.u_max : a.u_min;
-    const bool z = (v % NU) % 3 == 2;
-    return upper ? -(z ? a.fz_max : a.fxy_max) : (z ? a.fz_min : -a.fxy_max);
-}
-
 // gait_mask_wave per half: lane l < N of each half evaluates step l of its own instance
 __device__ __forceinline__ uint64_t gait_mask_half(int N, double Ts, double phase0, float swing,
                                                    float stance) {
@@ -111,10 +115,8 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     const bool valid = bq < a.B;
     const int b = valid ? bq : a.B - 1;  // the spare half of an odd batch re-reads the last QP
     double *D = reinterpret_cast<double *>(smem + (up ? Lay::bytes : 0));
-    double *xs = D + Lay::oXS;
     int *fid = reinterpret_cast<int *>(D + Lay::nDoubles);
     int *pos = fid + NF;
-    unsigned char *st = reinterpret_cast<unsigned char *>(pos + NV);
     double *X0 = D + Lay::oX0, *X1 = D + Lay::oX1, *Ax = D + Lay::oAx, *A2x = D + Lay::oA2x;
     double *xr = D + Lay::oXr, *x0g = D + Lay::oX0v, *UV = D + Lay::oUV;
     double *S = D + Lay::oS, *Rm = D + Lay::oRm;
@@ -137,7 +139,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         if (hl < NX) x0g[hl] = stv;
         if (hl < NRM) Rm[hl] = rm0;
         if (hl + kHalf < NRM) Rm[hl + kHalf] = rm1;
-        lin[0] = hread(stv, 2);
+        lin[0] = hbcast<2>(stv);
         if (hl < NX) {
 #pragma unroll
             for (int i = 0; i <= N; ++i) {
@@ -171,6 +173,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         if (hl + kHalf < NRM) Rm[hl + kHalf] = rm1;
     }
     wave_sync();
+    MPCQP_CUT(a.cut, 11);
 
     // ---- model: lane i < NX holds row i of Ac; X0 = Bc Ts and X1 = (Ac Ts) X0 on their
     //      support rows, A x0, A^2 x0 (A = Ac Ts).  Same products, in the same order, as the
@@ -212,6 +215,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         for (int k = 0; k < NX; ++k) s += arow[k] * Ax[k];
         A2x[hl] = s * Ts;
     }
+    MPCQP_CUT(a.cut, 13);
 
     // ---- free map and constraint states (gi_setup for generated bounds, no rows)
     int status = ST_OK, nf = 0;
@@ -234,16 +238,11 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         if (infeas) status = ST_INFEASIBLE;
         if (nf > NF) status = ST_BAD_DIMS;
     }
-    wave_sync();
-    if (status == ST_OK) {
-        for (int id = hl; id < 2 * nf; id += kHalf) {
-            double lo, hi;
-            pair_bound<NU, MODEL>(a, contact, fid[id < nf ? id : id - nf], lo, hi);
-            st[id] = (id < nf) ? (lo > -kInfty ? 1 : 0) : (hi < kInfty ? 1 : 0);
-        }
-    }
     if (nf > a.max_free) status = ST_BAD_DIMS;
+    uint64_t *ctl = reinterpret_cast<uint64_t *>(D + Lay::oCt);
+    if (hl == 0) *ctl = contact;  // reloaded for the outputs: nothing per instance stays live
     wave_sync();
+    MPCQP_CUT(a.cut, 1);
 
     // ---- S^W_rr = X_r' W X_r over the support rows (w: 0 = Q, 1 = P), entry o = cj NU + ci
 #pragma unroll
@@ -277,6 +276,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         UV[(m * 2 + 1) * NU + c] = sv;
     }
     wave_sync();
+    MPCQP_CUT(a.cut, 2);
 
     // ---- g (lane p: g_p), then H_FF over the dead early view (lane p loads row p)
     const bool ok = valid && status == ST_OK && nf > 0;
@@ -333,8 +333,9 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         h[q] = in ? Hb[lrow(hl) + q] : ((q == hl) ? 1.0 : 0.0);
     }
     wave_sync();
+    MPCQP_CUT(a.cut, 3);
 
-    // ---- solver (gi_run_reg with NF = 31 per half)
+    // ---- solver (gi_run_reg with NF = 30 per half)
     double *Lc = D + Lay::oR, *R = D + Lay::oR;
     double *rowbuf = D + Lay::oRow, *colb = rowbuf + NP, *rot = rowbuf + 2 * NP,
            *rinv = rowbuf + 4 * NP;
@@ -346,7 +347,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     bool ok2 = ok;
     if (any_ok) {
         // ---- Cholesky, right-looking, lane l owns row l (identity padding beyond nf)
-        double piv = hread(h[0], 0);
+        double piv = hbcast<0>(h[0]);
         bool bad = !(piv > 0.0);
         double ik = rsqrt_nr(piv);
 #pragma unroll
@@ -357,7 +358,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             if (hl == 0) rowbuf[k] = ik;
             double pivn = 1.0, ikn = 1.0;
             if (k + 1 < NF) {
-                pivn = hread(h[k + 1 < NF ? k + 1 : k] - lik * lik, k + 1);
+                pivn = hbcast(h[k + 1 < NF ? k + 1 : k] - lik * lik, k + 1);
                 bad |= !(pivn > 0.0);
                 ikn = rsqrt_nr(pivn);
             }
@@ -365,7 +366,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
 #pragma unroll
             for (int j = 0; j < NF; ++j) {
                 if (j > k) h[j] -= lik * Lc[ccol(k, NF) + j - k];
-                if ((j & 7) == 7 && j > k) step_fence();
+                if ((j % MPCQP_PF_CHOL) == MPCQP_PF_CHOL - 1 && j > k) step_fence();
             }
 #pragma unroll
             for (int j = 0; j < NF; ++j)
@@ -378,6 +379,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         }
         if (ok && bad) status = ST_NOT_PD;
         ok2 = ok && status == ST_OK;
+        MPCQP_CUT(a.cut, 4);
         // ---- columns of L^-1 (rows of J) in registers; lane 31 of each half solves L t = g
         if (hl < NF) colb[hl] = gv;
         wave_sync();
@@ -392,13 +394,14 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
 #pragma unroll
             for (int l = 0; l < NF; ++l) {
                 if (l > i) Jr[l] -= Lc[ccol(i, NF) + l - i] * Jr[i];
-                if ((l & 15) == 15 && l > i) step_fence();
+                if ((l % MPCQP_PF_INV) == MPCQP_PF_INV - 1 && l > i) step_fence();
             }
 #pragma unroll
             for (int l = 0; l < NF; ++l)
                 if (l >= i) pin(Jr[l]);
             step_fence();
         }
+        MPCQP_CUT(a.cut, 5);
         // ---- unconstrained minimum x = -J t, objective -|t|^2 / 2
         wave_sync();
         if (hl == kHalf - 1) {
@@ -411,37 +414,59 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
 #pragma unroll
         for (int j = 0; j < NF; ++j) {
             s4[j & 3] += Jr[j] * colb[j];
-            if ((j & 7) == 7) step_fence();
+            if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
         }
         x = (ok2 && hl < nf) ? -((s4[0] + s4[1]) + (s4[2] + s4[3])) : 0.0;
         fval = half_sum(hl < nf ? gv * gv : 0.0);
         fval = ok2 ? -0.5 * fval : 0.0;
-        if (ok2 && hl < nf) xs[hl] = x;
-        wave_sync();
     }
+    MPCQP_CUT(a.cut, 6);
 
-    // ---- dual active-set loop, flattened (one add or drop per pass); the wave runs while
-    //      either half has work
+    // ---- dual active-set loop (Goldfarb-Idnani), flattened: one add or drop per pass, the
+    //      wave running while either half has work.  Lane l owns variable l's two bound
+    //      constraints (ids l and l + nf): their b and eligibility live in registers, so the
+    //      most-violated search is register arithmetic plus one half-wave argmin.
+    //      Add step: J2 <- J2 (I - beta v v'), the Householder reflection that maps d2 to
+    //      |d2| e_q (v_q by Parlett's cancellation-free form).  It leaves the same first
+    //      column J2 d2 / |d2| and R column as the Givens chain of gi_reg.hpp / the oracle;
+    //      the trailing columns of J2 are another orthonormal basis of the same subspace, which
+    //      every later GI quantity (z = J2 J2' n, d1 = J1' n, r) is invariant to.  62 FMAs on
+    //      the resident rows instead of 30 rotations and their suffix-scan set-up.
+    //      Drop step: Givens restores R to triangular, the rotations go to LDS for J.
     const int mt = 2 * nf;
     const int max_iter = a.max_iter > 0 ? a.max_iter : 10 * (mt + nf + 1);
+    // bit 0 / 1: lower / upper bound inactive (eligible); bit 2: the variable is a vertical
+    // force.  A free variable is a force in contact (or a literal-model input), so its bounds
+    // follow from bit 2 alone: b of x >= lo is lo, b of -x >= -hi is -hi
+    int stb = 0;
+    if (ok2 && hl < nf) {
+        double lo, hi;
+        pair_bound<NU, MODEL>(a, contact, fid[hl], lo, hi);
+        stb = (lo > -kInfty ? 1 : 0) | (hi < kInfty ? 2 : 0) |
+              ((MODEL == 0 && (fid[hl] % NU) % 3 == 2) ? 4 : 0);
+    }
+    auto blo_of = [&](int sb) { return MODEL == 1 ? a.u_min : ((sb & 4) ? a.fz_min : -a.fxy_max); };
+    auto bhi_of = [&](int sb) { return MODEL == 1 ? -a.u_max : ((sb & 4) ? -a.fz_max : -a.fxy_max); };
     bool done = !ok2;
     bool fresh = true;
     int p = 0;
     while (__ballot(!done) != 0ull) {
-        double dj = 0.0, sp = 0.0, z = 0.0, zn = 0.0, r = 0.0, t1 = INFINITY, t2 = INFINITY;
-        double t = 0.0;
-        int kslot = 0x7fffffff;
+        double dj = 0.0, sp = 0.0, z = 0.0, zn = 0.0, zq = 0.0, r = 0.0, t1 = INFINITY,
+               t2 = INFINITY, t = 0.0, sg = 1.0, beta = 0.0;
+        int kslot = 0x7fffffff, a_ = 0;
+        bool lower = true;
         if (!done && fresh) {
             // ---- most violated inactive bound (lowest id on ties)
             double best = INFINITY;
             int bid = 0x7fffffff;
-            for (int id = hl; id < mt; id += kHalf) {
-                if (st[id] != 1) continue;
-                const bool lower = id < nf;
-                const int a_ = lower ? id : id - nf;
-                const double bb = pair_free_b<NU, MODEL>(a, fid[a_], !lower);
-                const double sl_ = (lower ? xs[a_] : -xs[a_]) - bb;
-                if (sl_ < -kFeasTol * (1.0 + fabs(bb)) && sl_ < best) { best = sl_; bid = id; }
+            const double blo = blo_of(stb), bhi = bhi_of(stb);
+            if (stb & 1) {
+                const double s_ = x - blo;
+                if (s_ < -kFeasTol * (1.0 + fabs(blo))) { best = s_; bid = hl; }
+            }
+            if (stb & 2) {
+                const double s_ = -x - bhi;
+                if (s_ < -kFeasTol * (1.0 + fabs(bhi)) && s_ < best) { best = s_; bid = hl + nf; }
             }
             half_argmin(best, bid);
             if (bid == 0x7fffffff) {
@@ -453,19 +478,24 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             }
         }
         if (!done) {
-            // ---- d = J' n_p (lane a's J row through LDS) and the slack of p
-            const bool lower = p < nf;
-            const int a_ = lower ? p : p - nf;
-            const double sg = lower ? 1.0 : -1.0;
-            const double bp = pair_free_b<NU, MODEL>(a, fid[a_], !lower);
+            // ---- d = J' n_p = sg J(a, :)': lane a publishes its J row twice (rowbuf: all of
+            //      d; colb: d with the active part j < q zeroed, for z) and the slack of p
+            lower = p < nf;
+            a_ = lower ? p : p - nf;
+            sg = lower ? 1.0 : -1.0;
             if (hl == a_) {
 #pragma unroll
-                for (int c = 0; c < NF; ++c) rowbuf[c] = Jr[c];
+                for (int c = 0; c < NF; ++c) {
+                    rowbuf[c] = Jr[c];
+                    colb[c] = Jr[c];
+                }
+                rowbuf[NP - 1] = lower ? x - blo_of(stb) : -x - bhi_of(stb);
             }
             wave_sync();
-            dj = (hl < nf) ? sg * rowbuf[hl] : 0.0;
-            sp = sg * xs[a_] - bp;
+            if (hl < q) colb[hl] = 0.0;
             wave_sync();
+            dj = (hl < nf) ? sg * rowbuf[hl] : 0.0;
+            sp = rowbuf[NP - 1];
             if (iters >= max_iter) { status = ST_ITER_LIMIT; done = true; }
         }
         const bool stepping = !done;
@@ -473,22 +503,21 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             ++iters;
             double dd = hl < nf ? dj * dj : 0.0;
             zn = (hl >= q && hl < nf) ? dj * dj : 0.0;
-            half_sum2(dd, zn);
-            colb[hl] = (hl >= q) ? dj : 0.0;
-            wave_sync();
+            zq = (hl > q && hl < nf) ? dj * dj : 0.0;
+            half_sum3(dd, zn, zq);
             double z4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int j = 0; j < NF; ++j) {
                 z4[j & 3] += Jr[j] * colb[j];
-                if ((j & 7) == 7) step_fence();
+                if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
             }
-            z = (z4[0] + z4[1]) + (z4[2] + z4[3]);
+            z = sg * ((z4[0] + z4[1]) + (z4[2] + z4[3]));
             // r = R^-1 d(0:q): uniform loop to the larger q of the two halves
             const int qmax = max(__builtin_amdgcn_readlane(q, 0), __builtin_amdgcn_readlane(q, kHalf));
             if (q > 0) {
                 double val = dj;
                 for (int j = qmax - 1; j >= 0; --j) {
-                    const double rj = hread(val, j) * rinv[j];
+                    const double rj = hread_rt(val, j) * rinv[j];
                     if (j < q) {
                         if (hl == j) r = rj;
                         if (hl < j) val -= R[roff(j) + hl] * rj;
@@ -508,33 +537,28 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         if (moving) {
             const double uq = hread_k(u, q);
             if (!isinf(t2)) {
-                if (hl < nf) { x += t * z; xs[hl] = x; }
+                if (hl < nf) x += t * z;
                 fval += t * zn * (0.5 * t + uq);
             }
             if (hl < q) u -= t * r;
             if (hl == q) u += t;
             add = !isinf(t2) && t2 <= t1;
             if (add) {
-                // ---- add p: the Givens chain's rotations from suffix sums of d^2
-                const double t0 = half_suffix_sum(hl < nf ? dj * dj : 0.0);
-                if (hl < NF) { colb[hl] = t0; rot[hl] = dj; }
-                wave_sync();
-                const double tm1 = (hl >= 1 && hl <= NF) ? colb[hl - 1] : t0;
-                const double dm1 = (hl >= 1 && hl <= NF) ? rot[hl - 1] : 0.0;
-                const double tp1 = (hl + 1 < NF) ? colb[hl + 1] : 0.0;
-                wave_sync();
-                const double accl = (tp1 == 0.0) ? dj : sqrt(t0);
-                double cl = 1.0, sl = 0.0;
-                if (hl > q && hl < nf && accl != 0.0) {
-                    const double ih = rsqrt_nr(tm1);
-                    cl = dm1 * ih;
-                    sl = accl * ih;
+                // ---- add p: R column q = (d_0..d_{q-1}, r_qq); the reflection vector v = d2
+                //      - |d2| e_q goes to colb (which holds d / sg), v = sg colb
+                const double dq = hread_k(dj, q);
+                double rqq = dq, vq = 0.0;
+                if (zq > 0.0) {  // otherwise d2 = d_q e_q: no reflection, r_qq = d_q
+                    const double nrm = sqrt(zn);
+                    rqq = nrm;
+                    vq = dq > 0.0 ? -zq / (dq + nrm) : dq - nrm;
+                    beta = 2.0 / (vq * vq + zq);
                 }
-                if (hl < NF) { rot[2 * hl] = cl; rot[2 * hl + 1] = sl; }
-                const double rqq = hread_k(accl, q);
+                wave_sync();
+                if (hl == q) colb[q] = sg * vq;
                 if (hl < q) R[roff(q) + hl] = dj;
                 if (hl == q) { R[roff(q) + q] = rqq; rinv[q] = 1.0 / rqq; act = p; }
-                if (hl == 0) st[p] = 2;
+                if (hl == a_) stb &= lower ? ~1 : ~2;
                 ++q;
                 fresh = true;
             } else {
@@ -542,7 +566,8 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 //      to triangular; the (c, s) pairs go to LDS for J
                 const int k = kslot;
                 const int dropped = hread_k(act, k);
-                if (hl == 0) st[dropped] = 1;
+                const bool dlow = dropped < nf;
+                if (hl == (dlow ? dropped : dropped - nf)) stb |= dlow ? 1 : 2;
                 {
                     const int src = (hl + 1 < kHalf) ? ln + 1 : ln;
                     const double un = __shfl(u, src, kWave);
@@ -589,47 +614,65 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             }
         }
         wave_sync();
-        // ---- the pass's rotations of J (add: pairs (j-1, j) bottom up; drop: (j, j+1))
-        if (moving && add) {
+        // ---- the pass's update of J, as ONE chain of wave-uniform steps (no divergent
+        //      definition of Jr, so the register allocator keeps a single copy of it):
+        //      add -> J2 (I - beta v v'), v = sg colb (the signs cancel: J_j -= beta (J . colb)
+        //      colb_j, f = 0 in a half that does not add); drop -> rotations (j, j+1) from LDS,
+        //      the identity in a half that does not drop
+        const bool hh = moving && add && beta != 0.0;
+        const bool rt = moving && !add;
+        if (__ballot(hh) != 0ull) {
+            double w4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int j = NF - 1; j >= 1; --j) {
-                const double c = rot[2 * j], s_ = rot[2 * j + 1];
-                const double y0 = Jr[j - 1], y1 = Jr[j];
-                Jr[j - 1] = c * y0 + s_ * y1;
-                Jr[j] = -s_ * y0 + c * y1;
-                if ((j & 7) == 0) step_fence();
+            for (int j = 0; j < NF; ++j) {
+                w4[j & 3] += Jr[j] * colb[j];
+                if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
+            }
+            const double f = hh ? beta * ((w4[0] + w4[1]) + (w4[2] + w4[3])) : 0.0;
+#pragma unroll
+            for (int j = 0; j < NF; ++j) {
+                Jr[j] -= f * colb[j];
+                if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
             }
         }
-        if (moving && !add) {
+        if (__ballot(rt) != 0ull) {
+            if (!rt) {
+                rot[2 * hl] = 1.0;
+                rot[2 * hl + 1] = 0.0;
+            }
+            wave_sync();
 #pragma unroll
             for (int j = 0; j < NF - 1; ++j) {
                 const double c = rot[2 * j], s_ = rot[2 * j + 1];
                 const double y0 = Jr[j], y1 = Jr[j + 1];
                 Jr[j] = c * y0 + s_ * y1;
                 Jr[j + 1] = -s_ * y0 + c * y1;
-                if ((j & 7) == 7) step_fence();
+                if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
             }
         }
         wave_sync();
     }
 
+    MPCQP_CUT(a.cut, 7);
     // ---- outputs
-    if (valid) {
-        double *U = a.U + (size_t)b * NV;
+    const int bo = 2 * (int)blockIdx.x + (upper_half() ? 1 : 0);
+    if (bo < a.B) {
+        const uint64_t cto = *ctl;
+        double *U = a.U + (size_t)bo * NV;
         const bool have_map = nf <= NF;
         for (int v = hl; v < NV; v += kHalf) {
             const int pv = pos[v];
             if (pv < 0 || !have_map) {
                 double lo, hi;
-                pair_bound<NU, MODEL>(a, contact, v, lo, hi);
+                pair_bound<NU, MODEL>(a, cto, v, lo, hi);
                 U[v] = (pv < 0) ? lo : 0.0;
             }
         }
         if (have_map && hl < nf) U[fid[hl]] = x;
         if (hl == 0) {
-            a.cost[b] = fval;
-            a.status[b] = status;
-            a.iters[b] = iters;
+            a.cost[bo] = fval;
+            a.status[bo] = status;
+            a.iters[bo] = iters;
         }
     }
     (void)NS;

@@ -10,7 +10,7 @@
 //   k_discretize<..>, k_condense_solve<..>   the batched hot path with compile-time dims
 //                (fused.hpp): linearise + expm, then Phi, H_FF, f and the solve in LDS
 //   k_mpc<..>, k_mpc_gen<..>   the whole tick in one kernel (mpc_fused.hpp), one QP per wave
-//   k_mpc_pair<..>             the same, two QPs per wave for nf <= 31 (mpc_pair.hpp)
+//   k_mpc_pair<..>             the same, two QPs per wave for nf <= 30 (mpc_pair.hpp)
 //                (instantiated in fast_srbm10 / fast_srbm20 / fast_literal / fast_pair.hip)
 //   k_select_min per-rank min-cost key (multi-GPU selection)
 //   k_plant      x <- Ad x + Bd u                                       src/QPSolver.cpp:108-111
@@ -727,7 +727,10 @@ int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
     return MPCQP_OK;
 }
 
-int mpcqp_ctx_fast_path(const mpcqp_ctx *c) { return c && c->fast ? 1 : 0; }
+int mpcqp_ctx_fast_path(const mpcqp_ctx *c) {
+    if (!c || !c->fast) return 0;
+    return c->fk.pair ? 2 : 1;
+}
 
 int mpcqp_debug_phase_cycles(mpcqp_ctx *c, uint64_t *out, int n) {
 #ifdef MPCQP_STAMPS

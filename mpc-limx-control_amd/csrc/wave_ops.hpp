@@ -128,102 +128,6 @@ __device__ __forceinline__ void wave_argmin(double &v, int &idx) { wave_arg<true
 // (value, index) maximum with the lowest index winning ties (Eigen maxCoeff semantics)
 __device__ __forceinline__ void wave_argmax(double &v, int &idx) { wave_arg<false>(v, idx); }
 
-// ---- half-wave primitives (two instances per wavefront: lanes 0-31 and 32-63).  Each half
-//      spans two whole 16-lane DPP rows, so the row-local DPP steps above never mix halves;
-//      the cross-row step reads the two rows of each half into SGPRs and selects per half.
-//      Reads of the other half's lanes ignore EXEC, so these also work inside a branch that
-//      only one half takes (the other half's result is discarded).
-constexpr int kHalf = 32;
-__device__ __forceinline__ bool upper_half() { return lane() >= kHalf; }
-
-// lane (half base + k) of each half; k wave-uniform
-__device__ __forceinline__ double hread(double v, int k) {
-    const double lo = readlane(v, k), hi = readlane(v, k + kHalf);
-    return upper_half() ? hi : lo;
-}
-__device__ __forceinline__ int hread(int v, int k) {
-    const int lo = readlane(v, k), hi = readlane(v, k + kHalf);
-    return upper_half() ? hi : lo;
-}
-// lane (half base + k) where k is uniform within each half (possibly different per half)
-__device__ __forceinline__ double hread_k(double v, int k) {
-    const int k0 = __builtin_amdgcn_readlane(k, 0) & (kHalf - 1);
-    const int k1 = __builtin_amdgcn_readlane(k, kHalf) & (kHalf - 1);
-    const double lo = readlane(v, k0), hi = readlane(v, k1 + kHalf);
-    return upper_half() ? hi : lo;
-}
-__device__ __forceinline__ int hread_k(int v, int k) {
-    const int k0 = __builtin_amdgcn_readlane(k, 0) & (kHalf - 1);
-    const int k1 = __builtin_amdgcn_readlane(k, kHalf) & (kHalf - 1);
-    const int lo = readlane(v, k0), hi = readlane(v, k1 + kHalf);
-    return upper_half() ? hi : lo;
-}
-// per-half ballot (bit i = lane base + i of this half)
-__device__ __forceinline__ uint32_t half_ballot(bool p) {
-    const uint64_t m = __ballot(p);
-    return upper_half() ? (uint32_t)(m >> 32) : (uint32_t)m;
-}
-__device__ __forceinline__ double row_sum(double v) {
-    v += dpp<kDppXor1>(v);
-    v += dpp<kDppXor2>(v);
-    v += dpp<kDppHalfMirror>(v);
-    v += dpp<kDppMirror>(v);
-    return v;
-}
-__device__ __forceinline__ double half_sum(double v) {
-    v = row_sum(v);
-    const double lo = readlane(v, 0) + readlane(v, 16), hi = readlane(v, 32) + readlane(v, 48);
-    return upper_half() ? hi : lo;
-}
-__device__ __forceinline__ void half_sum2(double &a, double &b) {
-    a += dpp<kDppXor1>(a);
-    b += dpp<kDppXor1>(b);
-    a += dpp<kDppXor2>(a);
-    b += dpp<kDppXor2>(b);
-    a += dpp<kDppHalfMirror>(a);
-    b += dpp<kDppHalfMirror>(b);
-    a += dpp<kDppMirror>(a);
-    b += dpp<kDppMirror>(b);
-    const bool up = upper_half();
-    const double alo = readlane(a, 0) + readlane(a, 16), ahi = readlane(a, 32) + readlane(a, 48);
-    const double blo = readlane(b, 0) + readlane(b, 16), bhi = readlane(b, 32) + readlane(b, 48);
-    a = up ? ahi : alo;
-    b = up ? bhi : blo;
-}
-__device__ __forceinline__ double half_max(double v) {
-    v = fmax(v, dpp<kDppXor1>(v));
-    v = fmax(v, dpp<kDppXor2>(v));
-    v = fmax(v, dpp<kDppHalfMirror>(v));
-    v = fmax(v, dpp<kDppMirror>(v));
-    const double lo = fmax(readlane(v, 0), readlane(v, 16)), hi = fmax(readlane(v, 32), readlane(v, 48));
-    return upper_half() ? hi : lo;
-}
-// lexicographic (value, index) minimum within each half
-__device__ __forceinline__ void half_argmin(double &v, int &idx) {
-    arg_step<kDppXor1, true>(v, idx);
-    arg_step<kDppXor2, true>(v, idx);
-    arg_step<kDppHalfMirror, true>(v, idx);
-    arg_step<kDppMirror, true>(v, idx);
-    const bool up = upper_half();
-    const double bv = up ? readlane(v, 32) : readlane(v, 0);
-    const int bi = up ? readlane(idx, 32) : readlane(idx, 0);
-    const double ov = up ? readlane(v, 48) : readlane(v, 16);
-    const int oi = up ? readlane(idx, 48) : readlane(idx, 16);
-    const bool take = ov < bv || (ov == bv && oi < bi);
-    v = take ? ov : bv;
-    idx = take ? oi : bi;
-}
-// inclusive suffix sum within each half: lane l gets sum_{i >= l, same half} v_i
-__device__ __forceinline__ double half_suffix_sum(double v) {
-    v += dpp_z<0x101>(v);
-    v += dpp_z<0x102>(v);
-    v += dpp_z<0x104>(v);
-    v += dpp_z<0x108>(v);
-    const double r1 = readlane(v, 16), r3 = readlane(v, 48);
-    const int row = lane() >> 4;
-    return v + (row == 0 ? r1 : (row == 2 ? r3 : 0.0));
-}
-
 // Ordering point between phases of a single-wave workgroup.  One wave issues its LDS
 // instructions in program order and the LDS executes them in order, so a store by one lane
 // is seen by a later load of another lane without any wait; only the compiler must not move

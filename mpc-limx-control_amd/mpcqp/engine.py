@@ -84,6 +84,13 @@ class BatchEngine:
     def fast_path(self) -> bool:
         return bool(lib().mpcqp_ctx_fast_path(self.ctx))
 
+    @property
+    def fused_kernel(self) -> str:
+        """name of the kernel mpcqp_batch_solve launches: k_mpc_pair (two QPs per wave),
+        k_mpc (one QP per wave) or the generic k_condense + k_solve pair"""
+        return {2: "k_mpc_pair", 1: "k_mpc"}.get(lib().mpcqp_ctx_fast_path(self.ctx),
+                                                  "k_condense+k_solve")
+
     def discretize(self, d, AB=None):
         """stage 1: linearise + exp(M Ts) -> [Ad | Bd] per instance"""
         t = self.torch

@@ -276,7 +276,7 @@ def test_generic_path_non_diagonal_weights(gpu, orc):
 
 
 def test_pair_kernel_matches_single_and_oracle(gpu, orc, monkeypatch):
-    """Two QPs per wavefront (csrc/mpc_pair.hpp, nf <= 31) against the one-QP-per-wave kernel
+    """Two QPs per wavefront (csrc/mpc_pair.hpp, nf <= 30) against the one-QP-per-wave kernel
     (MPCQP_PAIR=0) and the oracle: odd batch (the last wave's upper half is idle), contact
     masks with fewer stance forces (nf < 30, uneven iteration counts inside a wave) and with
     both feet down at one step (nf > max_free -> BAD_DIMS beside a solved neighbour)."""
