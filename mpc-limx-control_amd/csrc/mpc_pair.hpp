@@ -346,7 +346,20 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     const bool any_ok = __ballot(ok) != 0ull;
     bool ok2 = ok;
     if (any_ok) {
-        // ---- Cholesky, right-looking, lane l owns row l (identity padding beyond nf)
+        // ---- Cholesky fused with the inverse sweep.  Right-looking, lane l owns row l of H_FF
+        //      (identity padding beyond nf).  Step k's column of L, broadcast from LDS for the
+        //      trailing update, is also the operand of step k of the forward substitution
+        //      that turns lane c's e_c into column c of L^-1 (= row c of J, in registers): one
+        //      LDS read feeds two independent FMA streams.  Lane 31 of each half starts from g
+        //      instead and ends with t = L^-1 g.  Same operations in the same order as a
+        //      separate Cholesky then inverse sweep.
+        if (hl < NF) colb[hl] = gv;
+        wave_sync();
+#pragma unroll
+        for (int l = 0; l < NF; ++l) {
+            Jr[l] = (hl == l) ? 1.0 : 0.0;
+            Jr[l] = (hl == kHalf - 1) ? colb[l] : Jr[l];
+        }
         double piv = hbcast<0>(h[0]);
         bool bad = !(piv > 0.0);
         double ik = rsqrt_nr(piv);
@@ -355,22 +368,26 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             const double lik = h[k] * ik;
             h[k] = lik;
             if (hl >= k && hl < NF) Lc[ccol(k, NF) + hl - k] = lik;
-            if (hl == 0) rowbuf[k] = ik;
             double pivn = 1.0, ikn = 1.0;
             if (k + 1 < NF) {
                 pivn = hbcast(h[k + 1 < NF ? k + 1 : k] - lik * lik, k + 1);
                 bad |= !(pivn > 0.0);
                 ikn = rsqrt_nr(pivn);
             }
+            Jr[k] *= ik;
             wave_sync();
 #pragma unroll
             for (int j = 0; j < NF; ++j) {
-                if (j > k) h[j] -= lik * Lc[ccol(k, NF) + j - k];
+                if (j > k) {
+                    const double c = Lc[ccol(k, NF) + j - k];
+                    h[j] -= lik * c;
+                    Jr[j] -= c * Jr[k];
+                }
                 if ((j % MPCQP_PF_CHOL) == MPCQP_PF_CHOL - 1 && j > k) step_fence();
             }
 #pragma unroll
             for (int j = 0; j < NF; ++j)
-                if (j >= k) pin(h[j]);
+                if (j >= k) { pin(h[j]); pin(Jr[j]); }
             piv = pivn;
             ik = ikn;
             pin(piv);
@@ -380,27 +397,6 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         if (ok && bad) status = ST_NOT_PD;
         ok2 = ok && status == ST_OK;
         MPCQP_CUT(a.cut, 4);
-        // ---- columns of L^-1 (rows of J) in registers; lane 31 of each half solves L t = g
-        if (hl < NF) colb[hl] = gv;
-        wave_sync();
-#pragma unroll
-        for (int l = 0; l < NF; ++l) {
-            Jr[l] = (hl == l) ? 1.0 : 0.0;
-            Jr[l] = (hl == kHalf - 1) ? colb[l] : Jr[l];
-        }
-#pragma unroll
-        for (int i = 0; i < NF; ++i) {
-            Jr[i] *= rowbuf[i];
-#pragma unroll
-            for (int l = 0; l < NF; ++l) {
-                if (l > i) Jr[l] -= Lc[ccol(i, NF) + l - i] * Jr[i];
-                if ((l % MPCQP_PF_INV) == MPCQP_PF_INV - 1 && l > i) step_fence();
-            }
-#pragma unroll
-            for (int l = 0; l < NF; ++l)
-                if (l >= i) pin(Jr[l]);
-            step_fence();
-        }
         MPCQP_CUT(a.cut, 5);
         // ---- unconstrained minimum x = -J t, objective -|t|^2 / 2
         wave_sync();
