@@ -474,8 +474,9 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             }
         }
         if (!done) {
-            // ---- d = J' n_p = sg J(a, :)': lane a publishes its J row twice (rowbuf: all of
-            //      d; colb: d with the active part j < q zeroed, for z) and the slack of p
+            // ---- d = J' n_p = sg J(a, :)': lane a publishes its J row and the slack of p;
+            //      every lane reads its d_j, then lanes j < q zero their slot, leaving d2 (the
+            //      inactive part, for z and the reflection) in the buffer
             lower = p < nf;
             a_ = lower ? p : p - nf;
             sg = lower ? 1.0 : -1.0;
@@ -483,15 +484,14 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
 #pragma unroll
                 for (int c = 0; c < NF; ++c) {
                     rowbuf[c] = Jr[c];
-                    colb[c] = Jr[c];
                 }
                 rowbuf[NP - 1] = lower ? x - blo_of(stb) : -x - bhi_of(stb);
             }
             wave_sync();
-            if (hl < q) colb[hl] = 0.0;
-            wave_sync();
             dj = (hl < nf) ? sg * rowbuf[hl] : 0.0;
             sp = rowbuf[NP - 1];
+            if (hl < q) rowbuf[hl] = 0.0;  // after every lane's read (LDS keeps program order)
+            wave_sync();
             if (iters >= max_iter) { status = ST_ITER_LIMIT; done = true; }
         }
         const bool stepping = !done;
@@ -504,7 +504,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             double z4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int j = 0; j < NF; ++j) {
-                z4[j & 3] += Jr[j] * colb[j];
+                z4[j & 3] += Jr[j] * rowbuf[j];
                 if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
             }
             z = sg * ((z4[0] + z4[1]) + (z4[2] + z4[3]));
@@ -541,7 +541,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             add = !isinf(t2) && t2 <= t1;
             if (add) {
                 // ---- add p: R column q = (d_0..d_{q-1}, r_qq); the reflection vector v = d2
-                //      - |d2| e_q goes to colb (which holds d / sg), v = sg colb
+                //      - |d2| e_q goes to rowbuf (which holds d2 / sg), v = sg rowbuf
                 const double dq = hread_k(dj, q);
                 double rqq = dq, vq = 0.0;
                 if (zq > 0.0) {  // otherwise d2 = d_q e_q: no reflection, r_qq = d_q
@@ -551,7 +551,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                     beta = 2.0 / (vq * vq + zq);
                 }
                 wave_sync();
-                if (hl == q) colb[q] = sg * vq;
+                if (hl == q) rowbuf[q] = sg * vq;
                 if (hl < q) R[roff(q) + hl] = dj;
                 if (hl == q) { R[roff(q) + q] = rqq; rinv[q] = 1.0 / rqq; act = p; }
                 if (hl == a_) stb &= lower ? ~1 : ~2;
@@ -612,8 +612,8 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         wave_sync();
         // ---- the pass's update of J, as ONE chain of wave-uniform steps (no divergent
         //      definition of Jr, so the register allocator keeps a single copy of it):
-        //      add -> J2 (I - beta v v'), v = sg colb (the signs cancel: J_j -= beta (J . colb)
-        //      colb_j, f = 0 in a half that does not add); drop -> rotations (j, j+1) from LDS,
+        //      add -> J2 (I - beta v v'), v = sg rowbuf (the signs cancel: J_j -= beta (J .
+        //      rowbuf) rowbuf_j, f = 0 in a half that does not add); drop -> rotations from LDS,
         //      the identity in a half that does not drop
         const bool hh = moving && add && beta != 0.0;
         const bool rt = moving && !add;
@@ -621,13 +621,13 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             double w4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int j = 0; j < NF; ++j) {
-                w4[j & 3] += Jr[j] * colb[j];
+                w4[j & 3] += Jr[j] * rowbuf[j];
                 if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
             }
             const double f = hh ? beta * ((w4[0] + w4[1]) + (w4[2] + w4[3])) : 0.0;
 #pragma unroll
             for (int j = 0; j < NF; ++j) {
-                Jr[j] -= f * colb[j];
+                Jr[j] -= f * rowbuf[j];
                 if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
             }
         }
