@@ -11,19 +11,23 @@
 // Here every lane-parallel phase serves two instances for the same instruction count:
 //   * lane l of a half owns row l of H_FF / L and row l of J (30 columns in registers); lane
 //     31 of each half carries g through the inverse sweep (t = L^-1 g), as lane 63 does in
-//     gi_reg.hpp
+//     gi_reg.hpp; the Cholesky and the inverse sweep run fused (one LDS column read per step
+//     feeds both)
 //   * broadcasts are LDS reads at a per-half address (one address per half); cross-lane reads
-//     at a uniform index are v_readlane of both halves plus a select (wave_ops.hpp, half_*)
-//   * reductions: DPP inside each 16-lane row, then the half's two rows
+//     at a constant index are DPP row_newbcast + v_permlane16_swap (half_ops.hpp)
+//   * reductions: DPP inside each 16-lane row, then v_permlane16_swap across the half's rows
 //   * the dual loop runs while either half is active; each half's state (q, iterations,
-//     status, the selected constraint) lives in VGPRs and a finished half idles (EXEC-masked)
-// Same algorithm, constraint order, tolerances and arithmetic as fast_mpc + gi_run_reg, so
-// results and iteration counts match the one-QP kernel and the CPU oracle.
+//     status, the selected constraint) lives in VGPRs and a finished half idles (EXEC-masked);
+//     the bound states live in the owning lane's registers, the add step is a Householder
+//     reflection (see the loop)
+// Same algorithm, constraint order and tolerances as fast_mpc + gi_run_reg (the add step's
+// reflection differs from their Givens chain only in rounding), so results match the
+// one-QP kernel and the CPU oracle to rounding and iteration counts agree.
 //
-// LDS per instance (config B): 6.2 KB -- the early model terms keep only the support rows of
+// LDS per instance (config B): 5.6 KB -- the early model terms keep only the support rows of
 // X0 / X1 and no [Ac | Bc] copy, the condensed linear terms die before the packed H is built
-// over them, and the bounds' b are recomputed from the free map -- so three waves (six QPs)
-// per SIMD fit in 160 KB.
+// over them, and the bounds live in registers -- so three waves (six QPs) per SIMD fit in
+// 160 KB.
 #pragma once
 #include "half_ops.hpp"
 #include "mpc_fused.hpp"
