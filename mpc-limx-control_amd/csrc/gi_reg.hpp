@@ -9,6 +9,9 @@
 //     registers -- Jr[NF]; the unconstrained minimum is x = -J t, objective -|t|^2 / 2
 //   * R lives in LDS, column-major packed with one sub-diagonal slot per column (the drop
 //     step's Hessenberg entry), reusing the parked-L space: NF(NF+3)/2 doubles in total
+//   * an add step updates J by a Householder reflection (2 NF FMAs), a drop step by Givens
+//     rotations (as the oracle); the two differ from the oracle's Givens-chain add only in
+//     rounding
 //   * x is mirrored in LDS (xs) for the constraint sweeps, with the constraint states
 // All loops over columns are unrolled to NF with wave-uniform predicates, so every register
 // index is a compile-time constant (no scratch), and cross-lane reads are v_readlane with
@@ -215,9 +218,9 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
     }
     MPCQP_STAMP(C.stamps, 7, tst); MPCQP_CUT(C.cut, 6);
 
-    // ---- dual active-set loop, flattened: one pass = one step (add or drop).  J changes in
-    //      exactly one place per pass (a rotation sequence read from LDS), so the register
-    //      allocator sees a single loop-carried definition of Jr.
+    // ---- dual active-set loop, flattened: one pass = one step (add or drop).  J changes at
+    //      the end of the pass in wave-uniform code (a reflection for an add, a rotation
+    //      sequence read from LDS for a drop), so the register allocator keeps one copy of Jr.
     const int max_iter = P.max_iter > 0 ? P.max_iter : 10 * (mt + nf + 1);
     bool done = (status != ST_OK) || nf == 0;
     bool fresh = true;  // select a new violated constraint
@@ -248,7 +251,8 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         ++iters;
         double dd = ln < nf ? dj * dj : 0.0;
         double zn = (ln >= q && ln < nf) ? dj * dj : 0.0;
-        wave_sum2(dd, zn);
+        double zq = (ln > q && ln < nf) ? dj * dj : 0.0;  // |d2|^2 without d_q
+        wave_sum3(dd, zn, zq);
         if (ln < NF) colb[ln] = (ln >= q) ? dj : 0.0;  // d_j = 0 for j >= nf
         wave_sync();
         double z4[4] = {0.0, 0.0, 0.0, 0.0};
@@ -284,29 +288,24 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         if (ln < q) u -= t * r;
         if (ln == q) u += t;
         const bool add = !isinf(t2) && t2 <= t1;
+        double beta = 0.0;
         if (add) {
-            // ---- add p: Givens chain on d from the bottom up to q+1.  The chain's running
-            //      norm is the suffix norm of d, so every rotation (c_j, s_j) comes from
-            //      suffix sums of squares in parallel, lane j owning rotation j:
-            //        acc_j = d_j if T_{j+1} == 0 else sqrt(T_j),  T_j = sum_{i>=j} d_i^2
-            //        rotation j mixes (j-1, j): c = d_{j-1}/sqrt(T_{j-1}),
-            //        s = acc_j/sqrt(T_{j-1}) (identity when acc_j == 0)
-            const double t0 = wave_suffix_sum(ln < nf ? dj * dj : 0.0);
-            if (ln < NF) { colb[ln] = t0; rot[ln] = dj; }
-            wave_sync();
-            const double tm1 = (ln >= 1 && ln <= NF) ? colb[ln - 1] : t0;
-            const double dm1 = (ln >= 1 && ln <= NF) ? rot[ln - 1] : 0.0;
-            const double tp1 = (ln + 1 < NF) ? colb[ln + 1] : 0.0;
-            wave_sync();
-            const double accl = (tp1 == 0.0) ? dj : sqrt(t0);
-            double cl = 1.0, sl = 0.0;
-            if (ln > q && ln < nf && accl != 0.0) {
-                const double ih = rsqrt_nr(tm1);
-                cl = dm1 * ih;
-                sl = accl * ih;
+            // ---- add p: J2 <- J2 (I - beta v v'), the Householder reflection with
+            //      v = d2 - |d2| e_q (v_q by Parlett's cancellation-free form) that maps d2 to
+            //      |d2| e_q.  Same new column J2 d2 / |d2| and R column as the Givens chain;
+            //      the trailing columns are another orthonormal basis of the same subspace,
+            //      which every later GI quantity (z = J2 J2' n, d1 = J1' n, r) is invariant
+            //      to.  colb holds d2 (zeros below q); v differs from it only at q.
+            const double dq = readlane(dj, q);
+            double rqq = dq, vq = 0.0;
+            if (zq > 0.0) {  // otherwise d2 = d_q e_q: no reflection, r_qq = d_q
+                const double nrm = sqrt(zn);
+                rqq = nrm;
+                vq = dq > 0.0 ? -zq / (dq + nrm) : dq - nrm;
+                beta = 2.0 / (vq * vq + zq);
             }
-            if (ln < NF) { rot[2 * ln] = cl; rot[2 * ln + 1] = sl; }
-            const double rqq = readlane(accl, q);
+            wave_sync();
+            if (ln == q) colb[q] = vq;
             if (ln < q) L.R[roff(q) + ln] = dj;
             if (ln == q) { L.R[roff(q) + q] = rqq; rinv[q] = 1.0 / rqq; act = p; }
             if (ln == 0) L.st[p] = 2;
@@ -359,16 +358,22 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             }
         }
         wave_sync();
-        // ---- the pass's rotations of J: add -> pairs (j-1, j) for j = NF-1 .. 1,
-        //      drop -> pairs (j, j+1) for j = 0 .. NF-2; identity where (c, s) = (1, 0)
+        // ---- the pass's update of J: add -> the reflection (J_j -= beta (J . v) v_j),
+        //      drop -> rotations (j, j+1) for j = 0 .. NF-2, identity where (c, s) = (1, 0)
         if (add) {
+            if (beta != 0.0) {
+                double w4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int j = NF - 1; j >= 1; --j) {
-                const double c = rot[2 * j], s_ = rot[2 * j + 1];
-                const double x0 = Jr[j - 1], x1 = Jr[j];
-                Jr[j - 1] = c * x0 + s_ * x1;
-                Jr[j] = -s_ * x0 + c * x1;
-                if ((j & 7) == 0) step_fence();
+                for (int j = 0; j < NF; ++j) {
+                    w4[j & 3] += Jr[j] * colb[j];
+                    if ((j & 7) == 7) step_fence();
+                }
+                const double f = beta * ((w4[0] + w4[1]) + (w4[2] + w4[3]));
+#pragma unroll
+                for (int j = 0; j < NF; ++j) {
+                    Jr[j] -= f * colb[j];
+                    if ((j & 7) == 7) step_fence();
+                }
             }
         } else {
 #pragma unroll

@@ -88,6 +88,24 @@ __device__ __forceinline__ void wave_sum2(double &a, double &b) {
     a = (readlane(a, 0) + readlane(a, 16)) + (readlane(a, 32) + readlane(a, 48));
     b = (readlane(b, 0) + readlane(b, 16)) + (readlane(b, 32) + readlane(b, 48));
 }
+// three independent sums in one pass
+__device__ __forceinline__ void wave_sum3(double &a, double &b, double &c) {
+    a += dpp<kDppXor1>(a);
+    b += dpp<kDppXor1>(b);
+    c += dpp<kDppXor1>(c);
+    a += dpp<kDppXor2>(a);
+    b += dpp<kDppXor2>(b);
+    c += dpp<kDppXor2>(c);
+    a += dpp<kDppHalfMirror>(a);
+    b += dpp<kDppHalfMirror>(b);
+    c += dpp<kDppHalfMirror>(c);
+    a += dpp<kDppMirror>(a);
+    b += dpp<kDppMirror>(b);
+    c += dpp<kDppMirror>(c);
+    a = (readlane(a, 0) + readlane(a, 16)) + (readlane(a, 32) + readlane(a, 48));
+    b = (readlane(b, 0) + readlane(b, 16)) + (readlane(b, 32) + readlane(b, 48));
+    c = (readlane(c, 0) + readlane(c, 16)) + (readlane(c, 32) + readlane(c, 48));
+}
 __device__ __forceinline__ double wave_max(double v) {
     v = fmax(v, dpp<kDppXor1>(v));
     v = fmax(v, dpp<kDppXor2>(v));
