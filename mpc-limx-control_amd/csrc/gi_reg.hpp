@@ -323,37 +323,60 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                 const int an = __shfl(act, src, kWave);
                 if (ln >= k && ln < q) { u = un; act = an; }
             }
-            for (int j = k; j < q - 1; ++j) {
-                const double v = (ln <= j + 1) ? L.R[roff(j + 1) + ln] : 0.0;
-                wave_sync();
-                if (ln <= j + 1) L.R[roff(j) + ln] = v;
-                wave_sync();
+            // R's columns k+1.. move one left: lane l moves its own entries (rows <= j + 1 of
+            //      column j + 1), so no lane waits on another -- four columns per round trip
+            for (int j = k; j < q - 1; j += 4) {
+                double v[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    v[t] = (j + t < q - 1 && ln <= j + t + 1) ? L.R[roff(j + t + 1) + ln] : 0.0;
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    if (j + t < q - 1 && ln <= j + t + 1) L.R[roff(j + t) + ln] = v[t];
             }
             --q;
             if (ln < NF) { rot[2 * ln] = 1.0; rot[2 * ln + 1] = 0.0; }
             wave_sync();
-            for (int j = k; j < q; ++j) {
-                const double a = L.R[roff(j) + j], bb = L.R[roff(j) + j + 1];
-                if (bb != 0.0) {
-                    const double hh = sqrt(a * a + bb * bb);
-                    const double ih = 1.0 / hh;
-                    const double c = a * ih, s_ = bb * ih;
+            // Givens back to triangular.  Rotation j mixes rows j and j+1 of the columns
+            // l > j (lane l - j - 1).  Row j+1 is untouched until then (prefetchable from LDS);
+            // row j's entries are the previous rotation's second outputs, one lane up (DPP
+            // wave_shl), and the next pivot R(j+1, j+1) is lane 0's second output: the chain
+            // from one rotation to the next stays in registers.  Same arithmetic as the
+            // LDS round-trip form.
+            if (k < q) {
+                double carry = 0.0;  // row j of columns j+1+ln, after the previous rotation
+                {
+                    const int l = k + 1 + ln;
+                    carry = (l < q) ? L.R[roff(l) + k] : 0.0;
+                }
+                double a = L.R[roff(k) + k];
+                for (int j = k; j < q; ++j) {
                     const int l = j + 1 + ln;
-                    double r0 = 0.0, r1 = 0.0;
-                    if (l < q) { r0 = L.R[roff(l) + j]; r1 = L.R[roff(l) + j + 1]; }
-                    wave_sync();
-                    if (l < q) { L.R[roff(l) + j] = c * r0 + s_ * r1; L.R[roff(l) + j + 1] = -s_ * r0 + c * r1; }
-                    if (ln == 0) {
-                        L.R[roff(j) + j] = hh;
-                        L.R[roff(j) + j + 1] = 0.0;
-                        rinv[j] = ih;
-                        rot[2 * j] = c;
-                        rot[2 * j + 1] = s_;
+                    const double bb = L.R[roff(j) + j + 1];
+                    const double r1 = (l < q) ? L.R[roff(l) + j + 1] : 0.0;
+                    const double r0 = carry;
+                    double n1 = r1;
+                    if (bb != 0.0) {
+                        const double hh = sqrt(a * a + bb * bb);
+                        const double ih = 1.0 / hh;
+                        const double c = a * ih, s_ = bb * ih;
+                        n1 = -s_ * r0 + c * r1;
+                        if (l < q) {
+                            L.R[roff(l) + j] = c * r0 + s_ * r1;
+                            L.R[roff(l) + j + 1] = n1;
+                        }
+                        if (ln == 0) {
+                            L.R[roff(j) + j] = hh;
+                            L.R[roff(j) + j + 1] = 0.0;
+                            rinv[j] = ih;
+                            rot[2 * j] = c;
+                            rot[2 * j + 1] = s_;
+                        }
+                    } else {
+                        if (ln == 0) rinv[j] = 1.0 / a;  // the shifted column's diagonal as it is
                     }
-                    wave_sync();
-                } else {
-                    if (ln == 0) rinv[j] = 1.0 / a;  // the shifted column's diagonal as it is
-                    wave_sync();
+                    a = readlane(n1, 0);    // R(j+1, j+1) after this rotation
+                    carry = wave_next(n1);  // row j+1 of columns j+2+ln
                 }
             }
         }
