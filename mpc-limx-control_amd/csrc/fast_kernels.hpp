@@ -10,6 +10,9 @@
 #ifndef MPCQP_W32
 #define MPCQP_W32 3  // waves per SIMD the NF <= 32 fused kernel is register-budgeted for
 #endif
+#ifndef MPCQP_W64
+#define MPCQP_W64 2  // the same for NF = 64
+#endif
 #include "condense.hpp"
 #include "fused.hpp"
 #include "mpc_fused.hpp"
@@ -50,7 +53,7 @@ __global__ void __launch_bounds__(64) k_condense_solve(FastArgs a) {
 }
 
 template <int NU, int N, int MODEL, bool FRIC, int NF>
-__global__ void __launch_bounds__(64, (NF <= 32 ? MPCQP_W32 : 2)) k_mpc(MpcArgs a) {
+__global__ void __launch_bounds__(64, (NF <= 32 ? MPCQP_W32 : MPCQP_W64)) k_mpc(MpcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_m[];
     if ((int)blockIdx.x >= a.B) return;
     fast_mpc<NU, N, MODEL, FRIC, NF>(a, smem_m);
@@ -59,7 +62,7 @@ __global__ void __launch_bounds__(64, (NF <= 32 ? MPCQP_W32 : 2)) k_mpc(MpcArgs 
 // device-generated inputs: the same fused step, x0/xref/lin/contact
 // built on chip from per-state data, gait candidates and commands
 template <int NU, int N, int MODEL, bool FRIC, int NF>
-__global__ void __launch_bounds__(64, (NF <= 32 ? 3 : 2)) k_mpc_gen(MpcArgs a) {
+__global__ void __launch_bounds__(64, (NF <= 32 ? 3 : MPCQP_W64)) k_mpc_gen(MpcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_g[];
     if ((int)blockIdx.x >= a.B) return;
     fast_mpc<NU, N, MODEL, FRIC, NF, true>(a, smem_g);
