@@ -288,9 +288,12 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     if (ok && hl < nf) {
         const int vi = fid[hl], ki = vi / NU, ci = vi % NU;
         double s = 0.0;
-        for (int m = ki + 1; m <= N; ++m) {
-            const double beta = (double)(m - 1 - ki) + 0.5;
-            s += UV[(m * 2 + 0) * NU + ci] + beta * UV[(m * 2 + 1) * NU + ci];
+#pragma unroll
+        for (int m = 1; m <= N; ++m) {  // m > ki; unrolled so the loads issue together
+            if (m > ki) {
+                const double beta = (double)(m - 1 - ki) + 0.5;
+                s += UV[(m * 2 + 0) * NU + ci] + beta * UV[(m * 2 + 1) * NU + ci];
+            }
         }
         gp = 2.0 * s;
     }
@@ -306,22 +309,36 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             beta_sums(ki + 1, N - 1, ki, kj, c, si, sj, sij);
             const double bi = (double)(N - 1 - ki) + 0.5, bj = (double)(N - 1 - kj) + 0.5;
             const double bij = bi * bj;
-            int mi = 0, mj = 0;
+            // the free inputs of a step come in whole force triples (a foot in contact has
+            // all three components free: the fast path's bounds guarantee it), so the block
+            // is a set of 3x3 foot-pair sub-blocks with consecutive positions
+            constexpr int NFT = NU / 3;
+            static_assert(NU % 3 == 0, "inputs are force triples");
+            int pI[NFT], pJ[NFT];
 #pragma unroll
-            for (int cc = 0; cc < NU; ++cc) {
-                mi |= (pos[ki * NU + cc] >= 0) << cc;
-                mj |= (pos[kj * NU + cc] >= 0) << cc;
+            for (int s = 0; s < NFT; ++s) {
+                pI[s] = pos[ki * NU + 3 * s];
+                pJ[s] = pos[kj * NU + 3 * s];
             }
-            for (int ri = mi; ri; ri &= ri - 1) {
-                const int ci = __builtin_ctz(ri), pp = pos[ki * NU + ci];
-                for (int rj = mj; rj; rj &= rj - 1) {
-                    const int cj = __builtin_ctz(rj), qq = pos[kj * NU + cj];
-                    if (pp >= qq) {
-                        const double *So = S + (cj * NU + ci) * 4;
-                        double v = c * So[0] + sij * So[1];
-                        v += So[2] + bij * So[3];
-                        if (ki == kj) v += Rm[cj * NU + ci];
-                        Hb[lrow(pp) + qq] = 2.0 * v;
+#pragma unroll
+            for (int si = 0; si < NFT; ++si) {
+#pragma unroll
+                for (int sj = 0; sj < NFT; ++sj) {
+                    if (pI[si] < 0 || pJ[sj] < 0) continue;
+#pragma unroll
+                    for (int a3 = 0; a3 < 3; ++a3) {
+#pragma unroll
+                        for (int b3 = 0; b3 < 3; ++b3) {
+                            const int pp = pI[si] + a3, qq = pJ[sj] + b3;
+                            const int ci = 3 * si + a3, cj = 3 * sj + b3;
+                            if (pp >= qq) {
+                                const double *So = S + (cj * NU + ci) * 4;
+                                double v = c * So[0] + sij * So[1];
+                                v += So[2] + bij * So[3];
+                                if (ki == kj) v += Rm[cj * NU + ci];
+                                Hb[lrow(pp) + qq] = 2.0 * v;
+                            }
+                        }
                     }
                 }
             }
