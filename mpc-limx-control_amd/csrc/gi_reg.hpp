@@ -235,7 +235,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                 double b, sl_;
                 if (id < nf) { b = L.cb[id]; sl_ = L.xs[id] - b; }
                 else if (id < 2 * nf) { b = L.cb[id]; sl_ = -L.xs[id - nf] - b; }
-                else { b = gi_cons_b(C, id); sl_ = gi_cons_slack_lane(C, id); }  // friction
+                else { b = gi_cons_b(C, id); sl_ = gi_fric_nx_lane(C, id) - b; }  // friction
                 if (sl_ < -kFeasTol * (1.0 + fabs(b)) && sl_ < best) { best = sl_; bid = id; }
             }
             wave_argmin(best, bid);

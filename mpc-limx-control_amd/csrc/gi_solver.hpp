@@ -183,6 +183,21 @@ __device__ __forceinline__ double gi_cons_slack_lane(const GiCtx &C, int id) {
     return s - gi_cons_b(C, id);
 }
 
+// n'x of friction row id (id in [2nf, 2nf + nfric)) evaluated by ONE lane, without b: the
+// register solver's sweep computes b once and subtracts it itself
+__device__ __forceinline__ double gi_fric_nx_lane(const GiCtx &C, int id) {
+    const SolveProblem &P = *C.P;
+    const GiLds &L = C.L;
+    const int r = id - 2 * C.nf, ks = r >> 2, t = r & 3;
+    const int k = ks / P.nfeet, sft = ks % P.nfeet;
+    const int pz = L.pos[k * P.nu + 3 * sft + 2], pt = L.pos[k * P.nu + 3 * sft + (t >> 1)];
+    const double sg = (t & 1) ? 1.0 : -1.0;
+    double s = 0.0;
+    if (pz >= 0) s += P.mu * L.xs[pz];
+    if (pt >= 0) s += sg * L.xs[pt];
+    return s;
+}
+
 // d_j = (J' n_p)_j on lane j, and the slack n_p'x - b (uniform); x: lane i holds x_i
 __device__ __forceinline__ void gi_cons_project(const GiCtx &C, int id, double x, double &dj, double &sp) {
     const SolveProblem &P = *C.P;
