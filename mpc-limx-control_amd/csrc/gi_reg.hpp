@@ -225,18 +225,50 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
     bool done = (status != ST_OK) || nf == 0;
     bool fresh = true;  // select a new violated constraint
     int p = 0;
+    // Lane l evaluates the constraints of its own variable: its two bounds (ids l, l + nf)
+    // and, when it is the vertical force of a foot in contact, that foot-step's four friction
+    // rows (ids fbase .. fbase + 3).  A foot in contact has all three forces free (the fast
+    // path's bounds guarantee it), at consecutive positions l-2, l-1, l, so the rows' x comes
+    // from the two lanes below by DPP and their b is 0 (no fixed part): one LDS round trip for
+    // the states instead of a strided sweep with dependent position / mirror reads.  Same
+    // slack arithmetic, same (value, id) order as that sweep (gi_cons_b / gi_fric_nx_lane).
+    int fbase = -1;
+    if (C.nfric > 0 && status == ST_OK && ln < nf) {
+        const int v = L.fid[ln], k = v / P.nu, c = v % P.nu, sft = c / 3;
+        if (c % 3 == 2 && ((P.contact >> (2 * k + sft)) & 1ull))
+            fbase = 2 * nf + 4 * (k * P.nfeet + sft);
+    }
     while (!done) {
         if (fresh) {
             // ---- step 1: most violated inactive constraint (lowest id on ties)
             double best = INFINITY;
             int bid = 0x7fffffff;
-            for (int id = ln; id < mt; id += kWave) {
-                if (L.st[id] != 1) continue;
-                double b, sl_;
-                if (id < nf) { b = L.cb[id]; sl_ = L.xs[id] - b; }
-                else if (id < 2 * nf) { b = L.cb[id]; sl_ = -L.xs[id - nf] - b; }
-                else { b = gi_cons_b(C, id); sl_ = gi_fric_nx_lane(C, id) - b; }  // friction
-                if (sl_ < -kFeasTol * (1.0 + fabs(b)) && sl_ < best) { best = sl_; bid = id; }
+            if (ln < nf) {
+                const unsigned char s0 = L.st[ln], s1 = L.st[ln + nf];
+                const double b0 = L.cb[ln], b1 = L.cb[ln + nf];
+                if (s0 == 1) {
+                    const double sl_ = x - b0;
+                    if (sl_ < -kFeasTol * (1.0 + fabs(b0))) { best = sl_; bid = ln; }
+                }
+                if (s1 == 1) {
+                    const double sl_ = -x - b1;
+                    if (sl_ < -kFeasTol * (1.0 + fabs(b1)) && sl_ < best) { best = sl_; bid = ln + nf; }
+                }
+            }
+            if (C.nfric > 0) {
+                const double xm1 = wave_prev(x), xm2 = wave_prev(xm1);  // x_{l-1} (fy), x_{l-2} (fx)
+                if (fbase >= 0) {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        if (L.st[fbase + t] != 1) continue;
+                        const double sg = (t & 1) ? 1.0 : -1.0;
+                        double s = 0.0;
+                        s += P.mu * x;
+                        s += sg * ((t >> 1) ? xm1 : xm2);
+                        const double sl_ = s - 0.0;
+                        if (sl_ < -kFeasTol * (1.0 + fabs(0.0)) && sl_ < best) { best = sl_; bid = fbase + t; }
+                    }
+                }
             }
             wave_argmin(best, bid);
             if (bid == 0x7fffffff) break;  // optimal

@@ -63,6 +63,14 @@ __device__ __forceinline__ double wave_next(double v) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
+// lane l gets lane l - 1's value (DPP wave_shr:1, crosses rows; lane 0 gets 0)
+__device__ __forceinline__ double wave_prev(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), 0x138, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 // inclusive suffix sum over the wave: lane l gets sum_{i >= l} v_i.  row_shl 1,2,4,8 scans
 // each 16-lane row; the rows after this one are added from their totals (lanes 16, 32, 48).
 __device__ __forceinline__ double wave_suffix_sum(double v) {
