@@ -331,3 +331,35 @@ def test_pair_kernel_literal_model(gpu, orc, monkeypatch):
     ref = orc.srbm_batch(p, batch["x0"], batch["xref"], batch["lin"], batch["contact"])
     for i in range(B):
         assert u_close(pair["U"][i], ref["U"][i]), i
+
+
+def test_friction_rows_mixed_contact_vs_oracle(gpu, orc):
+    """Config C (friction pyramid) with double-support and flight steps mixed into the gait:
+    the one-QP solver evaluates each foot-step's four friction rows on the lane of its
+    vertical force (neighbours' forces by DPP), which must give the oracle's optimum and
+    iteration counts whatever the stance pattern (nf up to 64)."""
+    import mpcqp
+    p = mpcqp.model_params("C")
+    p["max_free"] = 64
+    B = 256
+    batch = mpcqp.make_batch(p, B, seed=21)
+    ct = batch["contact"].astype(np.uint64).copy()
+    rng = np.random.default_rng(4)
+    for i in range(B):
+        ks = rng.choice(p["N"], 3, replace=False)
+        ct[i] |= np.uint64(3 << (2 * int(ks[0])))      # double support
+        ct[i] &= ~np.uint64(3 << (2 * int(ks[1])))     # flight
+        if i % 2:
+            ct[i] |= np.uint64(3 << (2 * int(ks[2])))  # a second double-support step
+    nfree = np.array([3 * bin(int(c)).count("1") for c in ct])
+    keep = nfree <= 64
+    batch = {k: v[keep] for k, v in batch.items()}
+    batch["contact"] = ct[keep]
+    o = run_batch(p, batch)
+    ref = orc.srbm_batch(p, batch["x0"], batch["xref"], batch["lin"], batch["contact"])
+    np.testing.assert_array_equal(o["status"], ref["status"])
+    assert np.all(o["status"] == 0) and o["status"].size > 200
+    bad = [i for i in range(o["U"].shape[0]) if not u_close(o["U"][i], ref["U"][i])]
+    assert not bad, bad[:10]
+    np.testing.assert_allclose(o["cost"], ref["cost"], rtol=1e-9, atol=1e-9)
+    assert np.mean(o["iters"] == ref["iters"]) >= 0.99
