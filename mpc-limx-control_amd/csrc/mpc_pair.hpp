@@ -472,29 +472,9 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                t2 = INFINITY, t = 0.0, sg = 1.0, beta = 0.0;
         int kslot = 0x7fffffff, a_ = 0;
         bool lower = true;
-        if (!done && fresh) {
-            // ---- most violated inactive bound (lowest id on ties)
-            double best = INFINITY;
-            int bid = 0x7fffffff;
-            const double blo = blo_of(stb), bhi = bhi_of(stb);
-            if (stb & 1) {
-                const double s_ = x - blo;
-                if (s_ < -kFeasTol * (1.0 + fabs(blo))) { best = s_; bid = hl; }
-            }
-            if (stb & 2) {
-                const double s_ = -x - bhi;
-                if (s_ < -kFeasTol * (1.0 + fabs(bhi)) && s_ < best) { best = s_; bid = hl + nf; }
-            }
-            half_argmin(best, bid);
-            if (bid == 0x7fffffff) {
-                done = true;  // optimal
-            } else {
-                p = bid;
-                if (hl == q) u = 0.0;
-                fresh = false;
-            }
-        }
-        if (!done) {
+        // a pass either steps on the selected constraint p or (first pass) only selects
+        const bool go = !done && !fresh;
+        if (go) {
             // ---- d = J' n_p = sg J(a, :)': lane a publishes its J row and the slack of p;
             //      every lane reads its d_j, then lanes j < q zero their slot, leaving d2 (the
             //      inactive part, for z and the reflection) in the buffer
@@ -515,7 +495,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             wave_sync();
             if (iters >= max_iter) { status = ST_ITER_LIMIT; done = true; }
         }
-        const bool stepping = !done;
+        const bool stepping = go && !done;
         if (stepping) {
             ++iters;
             double dd = hl < nf ? dj * dj : 0.0;
@@ -631,12 +611,36 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             }
         }
         wave_sync();
+        if (!done && fresh) {
+            // ---- most violated inactive bound (lowest id on ties): before the first step and
+            //      right after every add, so a half's last add also ends its solve (no checking
+            //      pass of its own, no update of J that nothing reads)
+            double best = INFINITY;
+            int bid = 0x7fffffff;
+            const double blo = blo_of(stb), bhi = bhi_of(stb);
+            if (stb & 1) {
+                const double s_ = x - blo;
+                if (s_ < -kFeasTol * (1.0 + fabs(blo))) { best = s_; bid = hl; }
+            }
+            if (stb & 2) {
+                const double s_ = -x - bhi;
+                if (s_ < -kFeasTol * (1.0 + fabs(bhi)) && s_ < best) { best = s_; bid = hl + nf; }
+            }
+            half_argmin(best, bid);
+            if (bid == 0x7fffffff) {
+                done = true;  // optimal
+            } else {
+                p = bid;
+                if (hl == q) u = 0.0;
+                fresh = false;
+            }
+        }
         // ---- the pass's update of J, as ONE chain of wave-uniform steps (no divergent
         //      definition of Jr, so the register allocator keeps a single copy of it):
         //      add -> J2 (I - beta v v'), v = sg rowbuf (the signs cancel: J_j -= beta (J .
         //      rowbuf) rowbuf_j, f = 0 in a half that does not add); drop -> rotations from LDS,
         //      the identity in a half that does not drop
-        const bool hh = moving && add && beta != 0.0;
+        const bool hh = moving && add && beta != 0.0 && !done;
         const bool rt = moving && !add;
         if (__ballot(hh) != 0ull) {
             double w4[4] = {0.0, 0.0, 0.0, 0.0};
