@@ -45,6 +45,10 @@ namespace mpcqp {
 #ifndef MPCQP_PF_DUAL
 #define MPCQP_PF_DUAL 8
 #endif
+// Cholesky + inverse: two columns per LDS round trip (1) or one (0)
+#ifndef MPCQP_CHOL2
+#define MPCQP_CHOL2 1
+#endif
 
 constexpr int kPairNF = 30;  // free variables per instance; lane 31 of a half carries g
 
@@ -384,6 +388,58 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         double piv = hbcast<0>(h[0]);
         bool bad = !(piv > 0.0);
         double ik = rsqrt_nr(piv);
+#if MPCQP_CHOL2
+        // Two columns per LDS round trip: column k+1 is finished in registers from column
+        // k's broadcast entry L(k+1, k) (DPP, no LDS), then both columns are written and the
+        // trailing update reads them together.  Per element the operations and their order
+        // are those of two single-column steps (bitwise the same factor and J).
+        static_assert(NF % 2 == 0, "column pairs");
+#pragma unroll
+        for (int k = 0; k < NF; k += 2) {
+            const double lik = h[k] * ik;
+            h[k] = lik;
+            const double ck1 = hbcast(lik, k + 1);  // L(k+1, k)
+            h[k + 1] -= lik * ck1;                  // column k's update of column k+1
+            const double piv1 = hbcast(h[k + 1], k + 1);
+            bad |= !(piv1 > 0.0);
+            const double ik1 = rsqrt_nr(piv1);
+            const double lik1 = h[k + 1] * ik1;
+            h[k + 1] = lik1;
+            double pivn = 1.0, ikn = 1.0;
+            if (k + 2 < NF) {
+                const double hk2 = h[k + 2 < NF ? k + 2 : k] - lik * lik;  // on lane k+2
+                pivn = hbcast(hk2 - lik1 * lik1, k + 2);
+                bad |= !(pivn > 0.0);
+                ikn = rsqrt_nr(pivn);
+            }
+            if (hl >= k && hl < NF) Lc[ccol(k, NF) + hl - k] = lik;
+            if (hl >= k + 1 && hl < NF) Lc[ccol(k + 1, NF) + hl - k - 1] = lik1;
+            Jr[k] *= ik;
+            Jr[k + 1] -= ck1 * Jr[k];
+            Jr[k + 1] *= ik1;
+            wave_sync();
+#pragma unroll
+            for (int j = 0; j < NF; ++j) {
+                if (j > k + 1) {
+                    const double c0 = Lc[ccol(k, NF) + j - k];
+                    const double c1 = Lc[ccol(k + 1, NF) + j - k - 1];
+                    h[j] -= lik * c0;
+                    h[j] -= lik1 * c1;
+                    Jr[j] -= c0 * Jr[k];
+                    Jr[j] -= c1 * Jr[k + 1];
+                }
+                if ((j % 4) == 3 && j > k + 1) step_fence();
+            }
+#pragma unroll
+            for (int j = 0; j < NF; ++j)
+                if (j >= k) { pin(h[j]); pin(Jr[j]); }
+            piv = pivn;
+            ik = ikn;
+            pin(piv);
+            pin(ik);
+            step_fence();
+        }
+#else
 #pragma unroll
         for (int k = 0; k < NF; ++k) {
             const double lik = h[k] * ik;
@@ -415,6 +471,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             pin(ik);
             step_fence();
         }
+#endif
         if (ok && bad) status = ST_NOT_PD;
         ok2 = ok && status == ST_OK;
         MPCQP_CUT(a.cut, 4);
