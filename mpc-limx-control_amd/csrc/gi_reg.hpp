@@ -126,35 +126,54 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         double piv = readlane(h[0], 0);
         bool bad = !(piv > 0.0);
         double ik = rsqrt_nr(piv);
+        //      Columns go in pairs: column k+1 is finished in registers from column k's
+        //      broadcast entry L(k+1, k), so one LDS write -> read round trip serves two
+        //      columns.  Per element the operations and their order are those of two
+        //      single-column steps.
+        static_assert(NF % 2 == 0, "column pairs");
 #pragma unroll
-        for (int k = 0; k < NF; ++k) {
+        for (int k = 0; k < NF; k += 2) {
             // on lane k, h[k] is the pivot itself, so lik there is L(k,k) = piv / sqrt(piv)
             const double lik = h[k] * ik;
             h[k] = lik;
+            const double ck1 = readlane(lik, k + 1);  // L(k+1, k)
+            h[k + 1] -= lik * ck1;                    // column k's update of column k+1
+            const double piv1 = readlane(h[k + 1], k + 1);
+            bad |= !(piv1 > 0.0);
+            const double ik1 = rsqrt_nr(piv1);
+            const double lik1 = h[k + 1] * ik1;
+            h[k + 1] = lik1;
             if constexpr (!T63) {
                 const double tk = readlane(gv, k) * ik;
                 gv = (ln == k) ? tk : ((ln > k) ? gv - lik * tk : gv);
+                const double tk1 = readlane(gv, k + 1) * ik1;
+                gv = (ln == k + 1) ? tk1 : ((ln > k + 1) ? gv - lik1 * tk1 : gv);
             }
-            // column k of L (diagonal first) into LDS: the broadcast for this step's update
-            // and, kept, the operand of the inverse sweep; 1/L(k,k) beside it
-            if (ln >= k && ln < NF) Lc[ccol(k, NF) + ln - k] = lik;
-            if (ln == 0) rowbuf[k] = ik;
             double pivn = 1.0, ikn = 1.0;
-            if (k + 1 < NF) {
-                pivn = readlane(h[k + 1 < NF ? k + 1 : k] - lik * lik, k + 1);
+            if (k + 2 < NF) {
+                const double hk2 = h[k + 2 < NF ? k + 2 : k] - lik * lik;  // on lane k+2
+                pivn = readlane(hk2 - lik1 * lik1, k + 2);
                 bad |= !(pivn > 0.0);
                 ikn = rsqrt_nr(pivn);
             }
+            // columns k, k+1 of L (diagonal first) into LDS: the broadcasts for this step's
+            // update and, kept, the operands of the inverse sweep; 1/L(k,k) beside them
+            if (ln >= k && ln < NF) Lc[ccol(k, NF) + ln - k] = lik;
+            if (ln >= k + 1 && ln < NF) Lc[ccol(k + 1, NF) + ln - k - 1] = lik1;
+            if (ln == 0) { rowbuf[k] = ik; rowbuf[k + 1] = ik1; }
             wave_sync();
 #pragma unroll
             for (int j = 0; j < NF; ++j)
             {
-                if (j > k) h[j] -= lik * Lc[ccol(k, NF) + j - k];
-                if ((j & 7) == 7 && j > k) step_fence();  // bound the loads in flight
+                if (j > k + 1) {
+                    h[j] -= lik * Lc[ccol(k, NF) + j - k];
+                    h[j] -= lik1 * Lc[ccol(k + 1, NF) + j - k - 1];
+                }
+                if ((j & 3) == 3 && j > k + 1) step_fence();  // bound the loads in flight
             }
 #pragma unroll
             for (int j = 0; j < NF; ++j)
-                if (j >= k) pin(h[j]);  // step k's updates happen in step k
+                if (j >= k) pin(h[j]);  // the pair's updates happen in the pair's step
             if constexpr (!T63) pin(gv);
             piv = pivn;
             ik = ikn;
