@@ -36,18 +36,8 @@ namespace mpcqp {
 
 // LDS loads in flight per step of the unrolled sweeps (a code-motion fence every PF elements):
 // larger hides more LDS latency behind the FMAs, smaller bounds the registers the loads hold
-#ifndef MPCQP_PF_CHOL
-#define MPCQP_PF_CHOL 8
-#endif
-#ifndef MPCQP_PF_INV
-#define MPCQP_PF_INV 16
-#endif
 #ifndef MPCQP_PF_DUAL
 #define MPCQP_PF_DUAL 8
-#endif
-// Cholesky + inverse: two columns per LDS round trip (1) or one (0)
-#ifndef MPCQP_CHOL2
-#define MPCQP_CHOL2 1
 #endif
 
 constexpr int kPairNF = 30;  // free variables per instance; lane 31 of a half carries g
@@ -388,7 +378,6 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         double piv = hbcast<0>(h[0]);
         bool bad = !(piv > 0.0);
         double ik = rsqrt_nr(piv);
-#if MPCQP_CHOL2
         // Two columns per LDS round trip: column k+1 is finished in registers from column
         // k's broadcast entry L(k+1, k) (DPP, no LDS), then both columns are written and the
         // trailing update reads them together.  Per element the operations and their order
@@ -439,39 +428,6 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             pin(ik);
             step_fence();
         }
-#else
-#pragma unroll
-        for (int k = 0; k < NF; ++k) {
-            const double lik = h[k] * ik;
-            h[k] = lik;
-            if (hl >= k && hl < NF) Lc[ccol(k, NF) + hl - k] = lik;
-            double pivn = 1.0, ikn = 1.0;
-            if (k + 1 < NF) {
-                pivn = hbcast(h[k + 1 < NF ? k + 1 : k] - lik * lik, k + 1);
-                bad |= !(pivn > 0.0);
-                ikn = rsqrt_nr(pivn);
-            }
-            Jr[k] *= ik;
-            wave_sync();
-#pragma unroll
-            for (int j = 0; j < NF; ++j) {
-                if (j > k) {
-                    const double c = Lc[ccol(k, NF) + j - k];
-                    h[j] -= lik * c;
-                    Jr[j] -= c * Jr[k];
-                }
-                if ((j % MPCQP_PF_CHOL) == MPCQP_PF_CHOL - 1 && j > k) step_fence();
-            }
-#pragma unroll
-            for (int j = 0; j < NF; ++j)
-                if (j >= k) { pin(h[j]); pin(Jr[j]); }
-            piv = pivn;
-            ik = ikn;
-            pin(piv);
-            pin(ik);
-            step_fence();
-        }
-#endif
         if (ok && bad) status = ST_NOT_PD;
         ok2 = ok && status == ST_OK;
         MPCQP_CUT(a.cut, 4);
