@@ -39,6 +39,13 @@ namespace mpcqp {
 #ifndef MPCQP_PF_DUAL
 #define MPCQP_PF_DUAL 8
 #endif
+// Cholesky + inverse: columns per LDS round trip, and the fence period of its trailing update
+#ifndef MPCQP_CHOL_CB
+#define MPCQP_CHOL_CB 2
+#endif
+#ifndef MPCQP_CHOL_PF
+#define MPCQP_CHOL_PF 4
+#endif
 
 constexpr int kPairNF = 30;  // free variables per instance; lane 31 of a half carries g
 
@@ -378,46 +385,60 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         double piv = hbcast<0>(h[0]);
         bool bad = !(piv > 0.0);
         double ik = rsqrt_nr(piv);
-        // Two columns per LDS round trip: column k+1 is finished in registers from column
-        // k's broadcast entry L(k+1, k) (DPP, no LDS), then both columns are written and the
-        // trailing update reads them together.  Per element the operations and their order
-        // are those of two single-column steps (bitwise the same factor and J).
-        static_assert(NF % 2 == 0, "column pairs");
+        // CB columns per LDS round trip: columns k+1 .. k+CB-1 are finished in registers from
+        // the panel's DPP-broadcast entries L(k+c, k+c'), then the CB columns are written and
+        // the trailing update reads them together.  Per element the operations and their
+        // order are those of CB single-column steps (bitwise the same factor and J).
+        constexpr int CB = MPCQP_CHOL_CB;
+        static_assert(NF % CB == 0, "whole column panels");
 #pragma unroll
-        for (int k = 0; k < NF; k += 2) {
-            const double lik = h[k] * ik;
-            h[k] = lik;
-            const double ck1 = hbcast(lik, k + 1);  // L(k+1, k)
-            h[k + 1] -= lik * ck1;                  // column k's update of column k+1
-            const double piv1 = hbcast(h[k + 1], k + 1);
-            bad |= !(piv1 > 0.0);
-            const double ik1 = rsqrt_nr(piv1);
-            const double lik1 = h[k + 1] * ik1;
-            h[k + 1] = lik1;
+        for (int k = 0; k < NF; k += CB) {
+            double lk[CB], ikc[CB];
+            ikc[0] = ik;
+            lk[0] = h[k] * ik;
+            h[k] = lk[0];
+#pragma unroll
+            for (int c = 1; c < CB; ++c) {
+#pragma unroll
+                for (int c2 = 0; c2 < c; ++c2)
+                    h[k + c] -= lk[c2] * hbcast(lk[c2], k + c);  // panel column c2's update
+                const double pc = hbcast(h[k + c], k + c);
+                bad |= !(pc > 0.0);
+                ikc[c] = rsqrt_nr(pc);
+                lk[c] = h[k + c] * ikc[c];
+                h[k + c] = lk[c];
+            }
             double pivn = 1.0, ikn = 1.0;
-            if (k + 2 < NF) {
-                const double hk2 = h[k + 2 < NF ? k + 2 : k] - lik * lik;  // on lane k+2
-                pivn = hbcast(hk2 - lik1 * lik1, k + 2);
+            if (k + CB < NF) {
+                double hn = h[k + CB < NF ? k + CB : k];  // on lane k+CB
+#pragma unroll
+                for (int c = 0; c < CB - 1; ++c) hn -= lk[c] * lk[c];
+                pivn = hbcast(hn - lk[CB - 1] * lk[CB - 1], k + CB);
                 bad |= !(pivn > 0.0);
                 ikn = rsqrt_nr(pivn);
             }
-            if (hl >= k && hl < NF) Lc[ccol(k, NF) + hl - k] = lik;
-            if (hl >= k + 1 && hl < NF) Lc[ccol(k + 1, NF) + hl - k - 1] = lik1;
-            Jr[k] *= ik;
-            Jr[k + 1] -= ck1 * Jr[k];
-            Jr[k + 1] *= ik1;
+#pragma unroll
+            for (int c = 0; c < CB; ++c)
+                if (hl >= k + c && hl < NF) Lc[ccol(k + c, NF) + hl - k - c] = lk[c];
+#pragma unroll
+            for (int c = 0; c < CB; ++c) {
+#pragma unroll
+                for (int c2 = 0; c2 < c; ++c2) Jr[k + c] -= hbcast(lk[c2], k + c) * Jr[k + c2];
+                Jr[k + c] *= ikc[c];
+            }
             wave_sync();
 #pragma unroll
             for (int j = 0; j < NF; ++j) {
-                if (j > k + 1) {
-                    const double c0 = Lc[ccol(k, NF) + j - k];
-                    const double c1 = Lc[ccol(k + 1, NF) + j - k - 1];
-                    h[j] -= lik * c0;
-                    h[j] -= lik1 * c1;
-                    Jr[j] -= c0 * Jr[k];
-                    Jr[j] -= c1 * Jr[k + 1];
+                if (j >= k + CB) {
+                    double cv[CB];
+#pragma unroll
+                    for (int c = 0; c < CB; ++c) cv[c] = Lc[ccol(k + c, NF) + j - k - c];
+#pragma unroll
+                    for (int c = 0; c < CB; ++c) h[j] -= lk[c] * cv[c];
+#pragma unroll
+                    for (int c = 0; c < CB; ++c) Jr[j] -= cv[c] * Jr[k + c];
                 }
-                if ((j % 4) == 3 && j > k + 1) step_fence();
+                if ((j % MPCQP_CHOL_PF) == MPCQP_CHOL_PF - 1 && j >= k + CB) step_fence();
             }
 #pragma unroll
             for (int j = 0; j < NF; ++j)
