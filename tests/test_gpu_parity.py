@@ -293,9 +293,12 @@ def test_pair_kernel_matches_single_and_oracle(gpu, orc, monkeypatch):
         if i % 7 == 3:  # double support at one step: 33 free forces
             ct[i] |= np.uint64(3 << (2 * int(rng.integers(p["N"]))))
     batch["contact"] = ct
+    from mpcqp.engine import BatchEngine
     monkeypatch.setenv("MPCQP_PAIR", "0")
+    assert BatchEngine(p).fused_kernel == "k_mpc"
     single = run_batch(p, batch)
     monkeypatch.delenv("MPCQP_PAIR")
+    assert BatchEngine(p).fused_kernel == "k_mpc_pair"
     pair = run_batch(p, batch)
     nfree = np.array([3 * bin(int(c)).count("1") for c in ct])
     bad_dims = nfree > p["max_free"]
