@@ -40,6 +40,10 @@ namespace mpcqp {
 #define MPCQP_PF_DUAL 8
 #endif
 // Cholesky + inverse: columns per LDS round trip, and the fence period of its trailing update
+// pair instances by contact schedule within aligned groups of 16 (see pair_sorted_instance)
+#ifndef MPCQP_PAIR_SORT
+#define MPCQP_PAIR_SORT 1
+#endif
 #ifndef MPCQP_CHOL_CB
 #define MPCQP_CHOL_CB 2
 #endif
@@ -107,6 +111,55 @@ __device__ __forceinline__ uint64_t gait_mask_half(int N, double Ts, double phas
     return spread_even(left) | (spread_even(right) << 1);
 }
 
+// Which instance each half solves.  A wave runs its dual loop until BOTH halves are done, so
+// the halves should need the same number of iterations.  Instances are taken in aligned
+// groups of 16 (the gait candidates of one state in the batch layout), sorted by contact
+// schedule (the generated-input path: by gait phase within the cycle, which orders the
+// schedules), ties by index; wave w of the group gets ranks 2w' and 2w'+1.  Candidates of
+// one state with the same schedule are the same QP, so they land in the same wave.  Every
+// instance is still solved and written at its own index; only the pairing changes.
+// lane j of this lane's 16-lane row (DPP row_newbcast; j constant after unrolling)
+__device__ __forceinline__ int row_bcast_u32(int v, int j) {
+    switch (j) {
+#define MPCQP_RB(i) case i: return __builtin_amdgcn_update_dpp(0, v, 0x150 + i, 0xf, 0xf, false);
+        MPCQP_RB(0) MPCQP_RB(1) MPCQP_RB(2) MPCQP_RB(3) MPCQP_RB(4) MPCQP_RB(5) MPCQP_RB(6)
+        MPCQP_RB(7) MPCQP_RB(8) MPCQP_RB(9) MPCQP_RB(10) MPCQP_RB(11) MPCQP_RB(12) MPCQP_RB(13)
+        MPCQP_RB(14) MPCQP_RB(15)
+#undef MPCQP_RB
+        default: return 0;
+    }
+}
+template <bool GEN>
+__device__ __forceinline__ int pair_sorted_instance(const MpcArgs &a) {
+    const int ln = lane(), c = ln & 15;
+    const int g0 = (2 * (int)blockIdx.x) & ~15;
+    const int gn = a.B - g0 < 16 ? a.B - g0 : 16;
+    unsigned long long key = ~0ull;
+    if (c < gn) {
+        if constexpr (GEN) {
+            const double cyc = (double)(a.swing + a.stance);
+            key = (unsigned long long)__double_as_longlong(fmod(a.phase[g0 + c], cyc));
+        } else {
+            key = a.contact[g0 + c];
+        }
+    }
+    const int klo = (int)(key & 0xffffffffull), khi = (int)(key >> 32);
+    int rank = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {  // row_newbcast: key j of this 16-lane row
+        const unsigned lo = (unsigned)row_bcast_u32(klo, j);
+        const unsigned hi = (unsigned)row_bcast_u32(khi, j);
+        const unsigned long long kj = ((unsigned long long)hi << 32) | lo;
+        rank += (j < gn && (kj < key || (kj == key && j < c))) ? 1 : 0;
+    }
+    // ranks 2w' (lower half) and 2w'+1 (upper half), both read off lanes 0-15 (row 0)
+    const int r0 = (2 * (int)blockIdx.x) & 15;
+    const unsigned m0 = (unsigned)(__ballot(ln < 16 && c < gn && rank == r0) & 0xffffull);
+    const unsigned m1 = (unsigned)(__ballot(ln < 16 && c < gn && rank == r0 + 1) & 0xffffull);
+    const unsigned m = ln >= kHalf ? m1 : m0;
+    return m ? g0 + __builtin_ctz(m) : a.B;  // a.B: no instance (rank beyond a short group)
+}
+
 template <int NU, int N, int MODEL, bool GEN>
 __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) {
     static_assert(!GEN || MODEL == 0, "generated inputs are defined for the SRBM model");
@@ -116,7 +169,8 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     constexpr int NX = 13, NS = NX + NU, NF = kPairNF, NV = Lay::NV, SD = Lay::SD, NP = kHalf;
     const int ln = lane(), hl = ln & (kHalf - 1);
     const bool up = ln >= kHalf;
-    const int bq = 2 * (int)blockIdx.x + (up ? 1 : 0);
+    int bq = 2 * (int)blockIdx.x + (up ? 1 : 0);
+    if constexpr (MPCQP_PAIR_SORT && MODEL == 0) bq = pair_sorted_instance<GEN>(a);
     const bool valid = bq < a.B;
     const int b = valid ? bq : a.B - 1;  // the spare half of an odd batch re-reads the last QP
     double *D = reinterpret_cast<double *>(smem + (up ? Lay::bytes : 0));
@@ -245,7 +299,10 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     }
     if (nf > a.max_free) status = ST_BAD_DIMS;
     uint64_t *ctl = reinterpret_cast<uint64_t *>(D + Lay::oCt);
-    if (hl == 0) *ctl = contact;  // reloaded for the outputs: nothing per instance stays live
+    if (hl == 0) {  // reloaded for the outputs: nothing per instance stays live
+        ctl[0] = contact;
+        ctl[1] = (uint64_t)(valid ? bq : -1);
+    }
     wave_sync();
     MPCQP_CUT(a.cut, 1);
 
@@ -710,8 +767,8 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
 
     MPCQP_CUT(a.cut, 7);
     // ---- outputs
-    const int bo = 2 * (int)blockIdx.x + (upper_half() ? 1 : 0);
-    if (bo < a.B) {
+    const int bo = (int)(long long)ctl[1];
+    if (bo >= 0) {
         const uint64_t cto = *ctl;
         double *U = a.U + (size_t)bo * NV;
         const bool have_map = nf <= NF;
