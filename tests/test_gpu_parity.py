@@ -318,6 +318,42 @@ def test_pair_kernel_matches_single_and_oracle(gpu, orc, monkeypatch):
     assert len(set(pair["iters"][ok].tolist())) > 2  # uneven work inside the waves
 
 
+def test_pair_kernel_full_size_vs_single(gpu, monkeypatch):
+    """metric batch (65536): the paired kernel's schedule-sorted instance assignment writes
+    every instance exactly once (outputs pre-filled with sentinels) and agrees with the
+    one-QP kernel everywhere: status and iteration counts equal, U / cost to 1e-12."""
+    import torch
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("B")
+    B = 65536
+    batch = mpcqp.make_batch(p, B, seed=23)
+    res = {}
+    for pair in (False, True):
+        if pair:
+            monkeypatch.delenv("MPCQP_PAIR", raising=False)
+        else:
+            monkeypatch.setenv("MPCQP_PAIR", "0")
+        eng = BatchEngine(p)
+        assert eng.fused_kernel == ("k_mpc_pair" if pair else "k_mpc")
+        d = eng.upload(batch)
+        d["U"].fill_(float("nan"))
+        d["cost"].fill_(float("nan"))
+        d["status"].fill_(99)
+        d["iters"].fill_(-1)
+        torch.cuda.synchronize()
+        eng.solve(d)
+        eng.sync()
+        res[pair] = {k: d[k].cpu().numpy().copy() for k in ("U", "cost", "status", "iters")}
+        eng.close()
+    a, b = res[True], res[False]
+    assert np.all(a["status"] == 0) and np.all(b["status"] == 0)
+    assert np.all(np.isfinite(a["U"])) and np.all(np.isfinite(a["cost"]))
+    np.testing.assert_array_equal(a["iters"], b["iters"])
+    np.testing.assert_allclose(a["U"], b["U"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(a["cost"], b["cost"], rtol=1e-12, atol=1e-12)
+
+
 def test_pair_kernel_literal_model(gpu, orc, monkeypatch):
     """reference-literal 13/3/10 (nf = 30) through the paired kernel vs the one-QP kernel"""
     import mpcqp
