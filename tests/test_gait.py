@@ -64,6 +64,33 @@ def test_solve_gait_matches_explicit(gpu, cfg):
 
 
 @pytest.mark.gpu
+def test_solve_gait_metric_batch_matches_explicit(gpu):
+    """metric batch (4096 states x 16 candidates = 65536): the on-chip generated path writes
+    every instance (outputs pre-filled with sentinels) and equals the explicit-input path"""
+    import torch
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("B")
+    g = mpcqp.make_gait_states(p, 4096, seed=29, candidates=16)
+    eng = BatchEngine(p)
+    dg = eng.upload_gait(g)
+    dg["U"].fill_(float("nan"))
+    dg["status"].fill_(99)
+    torch.cuda.synchronize()
+    eng.solve_gait(dg)
+    d = eng.upload(mpcqp.gait_inputs(p, g))
+    eng.solve(d)
+    eng.sync()
+    st = dg["status"].cpu().numpy()
+    assert st.shape == (65536,) and np.all(st == 0)
+    np.testing.assert_array_equal(st, d["status"].cpu().numpy())
+    np.testing.assert_allclose(dg["U"].cpu().numpy(), d["U"].cpu().numpy(), rtol=0, atol=1e-10)
+    np.testing.assert_allclose(dg["cost"].cpu().numpy(), d["cost"].cpu().numpy(), rtol=1e-12,
+                               atol=1e-12)
+    eng.close()
+
+
+@pytest.mark.gpu
 def test_plant_srbm_matches_oracle(gpu, orc):
     import mpcqp
     from mpcqp.engine import BatchEngine
