@@ -158,9 +158,17 @@ __device__ __forceinline__ unsigned long long order_bits(float c) {
     return (u & 0x80000000u) ? (unsigned long long)(~u) : (unsigned long long)(u | 0x80000000u);
 }
 
+// One launch: each block reduces its grid-stride share to a partial key, the last block to
+// finish (ticket from a device-scope counter) reduces the partials into *key and re-arms the
+// counter for the next call on this context's stream.  No pre-fill launch of the key; an
+// empty batch (B = 0, one block) yields the no-valid-instance key 0x7fffffffffffffff.
+constexpr int kSelMaxBlocks = 1024;
 __global__ void __launch_bounds__(256) k_select_min(int B, const double *cost, const int *status,
-                                                     long long base, unsigned long long *key) {
+                                                     long long base, unsigned long long *key,
+                                                     unsigned long long *partial,
+                                                     unsigned int *ticket) {
     __shared__ unsigned long long red[4];
+    __shared__ bool last;
     unsigned long long best = 0x7fffffffffffffffull;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B; i += gridDim.x * blockDim.x) {
         if (status[i] != 0) continue;
@@ -178,11 +186,34 @@ __global__ void __launch_bounds__(256) k_select_min(int B, const double *cost, c
     if (threadIdx.x == 0) {
         unsigned long long m = red[0];
         for (int w = 1; w < (int)(blockDim.x >> 6); ++w) m = red[w] < m ? red[w] : m;
-        atomicMin(key, m);
+        __hip_atomic_store(&partial[blockIdx.x], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        last = t == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    best = 0x7fffffffffffffffull;
+    for (int b = threadIdx.x; b < (int)gridDim.x; b += blockDim.x) {
+        const unsigned long long v =
+            __hip_atomic_load(&partial[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        best = v < best ? v : best;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long t = __shfl_xor(best, o, 64);
+        best = t < best ? t : best;
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long m = red[0];
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) m = red[w] < m ? red[w] : m;
+        *key = m;
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
-
-__global__ void k_fill_u64(unsigned long long *p, unsigned long long v) { *p = v; }
 
 __global__ void __launch_bounds__(64) k_plant(int nx, int nu, const double *Ad, const double *Bd,
                                               double *x, const double *u) {
@@ -439,6 +470,7 @@ struct mpcqp_ctx {
     double *dAB = nullptr;                  // [B][nx*(nx+nu)] discretised model scratch
     size_t ab_cap = 0;
     unsigned long long *dstamps = nullptr;  // diagnostic phase cycles (stamps build)
+    unsigned long long *dsel = nullptr;     // k_select_min: per-block partial keys + ticket
     // host-pointer entry point staging
     void *hbuf = nullptr;
     size_t hbuf_cap = 0;
@@ -707,6 +739,8 @@ int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
         hipMemcpy(c->dP, m->P, sizeof(double) * nx * nx, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->dqd, qd, sizeof(double) * nx, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->dpd, pd, sizeof(double) * nx, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMalloc(&c->dsel, sizeof(unsigned long long) * (kSelMaxBlocks + 1)) != hipSuccess ||
+        hipMemset(c->dsel, 0, sizeof(unsigned long long) * (kSelMaxBlocks + 1)) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         mpcqp_ctx_destroy(c);
         return MPCQP_ERR_DEVICE;
@@ -767,6 +801,7 @@ int mpcqp_ctx_destroy(mpcqp_ctx *c) {
     hipFree(c->dpd);
     hipFree(c->dAB);
     hipFree(c->dstamps);
+    hipFree(c->dsel);
     hipFree(c->hbuf);
     hipFree(c->rbuf);
     hipFree(c->scratchH);
@@ -1209,12 +1244,10 @@ int mpcqp_batch_select_min(mpcqp_ctx *c, int B, const double *cost, const int *s
     if (!c || !cost || !status || !key || B < 0) return MPCQP_ERR_BAD_ARG;
     hipSetDevice(c->device);
     unsigned long long *k = reinterpret_cast<unsigned long long *>(key);
-    hipLaunchKernelGGL(k_fill_u64, dim3(1), dim3(1), 0, c->stream, k, 0x7fffffffffffffffull);
-    if (B > 0) {
-        const int blocks = std::min(1024, (B + 255) / 256);
-        hipLaunchKernelGGL(k_select_min, dim3(blocks), dim3(256), 0, c->stream, B, cost, status,
-                           (long long)index_base, k);
-    }
+    const int blocks = std::max(1, std::min(kSelMaxBlocks, (B + 255) / 256));
+    hipLaunchKernelGGL(k_select_min, dim3(blocks), dim3(256), 0, c->stream, B, cost, status,
+                       (long long)index_base, k, c->dsel,
+                       reinterpret_cast<unsigned int *>(c->dsel + kSelMaxBlocks));
     return hip_status(hipGetLastError());
 }
 
