@@ -180,7 +180,9 @@ int mpcqp_batch_solve_host(mpcqp_ctx *ctx, int B, const double *x0, const double
 
 /* key = (order-preserving bits of (float)cost << 31) | (index_base + i), min over the batch,
  * written to *key (device int64).  Instances with status != OK never win.  The caller
- * reduces keys across ranks with one MIN all-reduce (RCCL). */
+ * reduces keys across ranks with one MIN all-reduce (RCCL).  One launch on the context's
+ * stream, using a context-owned partial-key buffer: calls on one context must stay ordered
+ * (the same stream, or a synchronisation after mpcqp_set_stream). */
 int mpcqp_batch_select_min(mpcqp_ctx *ctx, int B, const double *cost, const int *status,
                            int64_t index_base, int64_t *key);
 
