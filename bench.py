@@ -243,6 +243,8 @@ def main():
                           algorithmic_bytes_per_launch=algorithmic_bytes(
                               p["nx"], p["nu"], p["N"]) * B,
                           algorithmic_flops_per_qp=f_qp,
+                          basis="SURVEY.md 8d algorithmic flops (F_fixed + F_iter x mean iters); "
+                                "the closed-form path executes fewer, so frac can exceed 1",
                           whole_step_tflops=dom_flops / (ms_per_step * 1e-3) / 1e12),
         )
         out["config"]["pcie_inclusive_qps"] = host_staged_rate(eng, batch, p)

@@ -1241,7 +1241,7 @@ int mpcqp_rollout(mpcqp_ctx *c, int S, int C, int K, double *state, double *feet
 
 int mpcqp_batch_select_min(mpcqp_ctx *c, int B, const double *cost, const int *status,
                            int64_t index_base, int64_t *key) {
-    if (!c || !cost || !status || !key || B < 0) return MPCQP_ERR_BAD_ARG;
+    if (!c || !key || B < 0 || (B > 0 && (!cost || !status))) return MPCQP_ERR_BAD_ARG;
     hipSetDevice(c->device);
     unsigned long long *k = reinterpret_cast<unsigned long long *>(key);
     const int blocks = std::max(1, std::min(kSelMaxBlocks, (B + 255) / 256));

@@ -216,6 +216,34 @@ def test_full_size_metric_batch_properties(gpu, orc):
         assert u_close(U1[i], ref["U"][j]), i
 
 
+def test_select_min_repeated_calls(gpu):
+    """k_select_min reduces in one launch (last block re-arms the context's ticket): repeated
+    calls on one context with different batch sizes (1 .. 1024 blocks, B = 0), index bases and
+    failed instances each return the host key"""
+    import torch
+    import mpcqp
+    from mpcqp.engine import BatchEngine, encode_key
+    p = mpcqp.model_params("B")
+    eng = BatchEngine(p)
+    rng = np.random.default_rng(17)
+    dev = torch.device("cuda:0")
+    key = torch.zeros(1, dtype=torch.int64, device=dev)
+    for B in (0, 1, 255, 256, 257, 4096, 65536, 300000, 3):
+        cost = rng.normal(size=B) * 100.0
+        status = np.where(rng.random(B) < 0.1, 3, 0).astype(np.int32)
+        base = int(rng.integers(0, 1 << 20))
+        d = dict(B=B, cost=torch.tensor(cost, device=dev),
+                 status=torch.tensor(status, device=dev), key=key)
+        torch.cuda.synchronize()
+        k = eng.select_min(d, index_base=base)
+        eng.sync()
+        got = int(k.item())
+        ok = np.nonzero(status == 0)[0]
+        want = min((encode_key(cost[i], base + int(i)) for i in ok), default=0x7FFFFFFFFFFFFFFF)
+        assert got == want, B
+    eng.close()
+
+
 def test_edge_cases(gpu):
     """empty batch, infeasible bounds, no free variable, non-PD Hessian, too many free vars"""
     from mpcqp.qpsolver import solve_dense
