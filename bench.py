@@ -1,21 +1,34 @@
 #!/usr/bin/env python3
 """Benchmark: QP solves/s for the TRON1 13-state / 6-input / N=10 SRBM MPC (BASELINE.json
-metric), batch 65,536 per GPU, 1..8 MI355X (one process per GPU, weak scaling: config D is
-524,288 = 65,536 x 8).
+metric): global batch 65,536 on 1/2/4/8 MI355X, STRONG scaling (65,536/N instances per GPU),
+one process per GPU.  Config D (weak scaling, 65,536 per GPU: 524,288 on 8 GPUs) is reported
+beside it in `config.weak`; the other single-GPU configs (B@4,096, C, L, standing/double
+support) in `config.per_config` (N = 1 only).
 
-One step = one pass of the hot path over the whole per-GPU batch, inputs resident in HBM:
+One step = one pass of the hot path over the rank's shard, inputs resident in HBM:
   k_mpc_pair (linearise + discretise + condense + Goldfarb-Idnani solve, fused, two QPs per
-  wavefront; k_mpc, one QP per wavefront, where nf > 30) -> k_select_min (min-cost key)
-  -> [N>1] RCCL MIN all-reduce of the 8-byte key + broadcast of the winner's U (480 B).
+  wavefront) -> k_select_min (per-rank selection record [min key | winner's U])
+  -> [N>1] ONE RCCL all-gather of the records (8 + 480 B per rank) -> k_reduce_records.
+No host synchronisation inside the step.
 
-Prints ONE JSON line on rank 0 (driver contract).
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config B|C|L]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--global-batch G] [--config B|C|L]
+
+`--gpus N` with N > 1 and no WORLD_SIZE in the environment launches N ranks itself
+(`python -m torch.distributed.run --nproc-per-node N ...` as a child process; this parent makes
+no GPU call).  Under torchrun (the driver's launch) RANK/LOCAL_RANK/WORLD_SIZE come from the
+environment.  Rank 0 prints ONE JSON line (driver contract; DESIGN.md sections 5-6).
+
+`--selection-dry-run` (test harness, CPU): the solve is replaced by seeded synthetic
+cost/status/U per shard and the ranks run the same launcher, sharding and one-collective
+selection over gloo; tests/test_bench_launcher.py checks n_gpus and the global argmin.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -25,6 +38,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "mpc-limx-control_amd"))
 
 FP64_PEAK_TFLOPS = 78.6  # MI355X dense FP64 (vector = matrix), AMD spec; SURVEY.md 8d
+METRIC = "QP solves/sec, 13-state N=10 SRBM MPC, batch=65536 at 1/2/4/8 MI355X"
+CANDIDATES = 16  # gait candidates per state: shards are aligned to whole states
 
 
 def algorithmic_flops(nx: int, nu: int, N: int):
@@ -49,51 +64,109 @@ def algorithmic_bytes(nx: int, nu: int, N: int):
     return (nx + nx * (N + 1) + 7 + 2 * N + nV + 1) * 8 + 4
 
 
+def flops_per_qp(p, mean_iters):
+    fl = algorithmic_flops(p["nx"], p["nu"], p["N"])
+    return fl["condense"] + fl["solve_fixed"] + fl["per_iter"] * float(mean_iters)
+
+
+def _profile_json(name):
+    try:
+        return json.load(open(os.path.join(ROOT, "profiles", name)))
+    except (OSError, ValueError):
+        return None
+
+
 def pmc_traffic(config: str, batch: int):
     """HBM bytes per fused-kernel launch from the committed rocprofv3 PMC summary
     (tools/profile_run.sh + tools/summarize_profile.py), if it matches this workload."""
-    try:
-        t = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
-    except (OSError, ValueError):
-        return None, None
-    if t.get("config") != config or t.get("batch") != batch:
+    t = _profile_json("pmc_traffic.json")
+    if not t or t.get("config") != config or t.get("batch") != batch:
         return None, None
     return t.get("hbm_bytes_per_launch"), t.get("tag")
 
 
+def pmc_executed(config: str, batch: int):
+    """Executed FP64 work of the fused kernel from the committed PMC pass
+    (SQ_INSTS_VALU_{FMA,MUL,ADD}_F64 and MFMA ops; tools/pmc_flops.sh), if it matches."""
+    t = _profile_json("pmc_flops.json")
+    if not t or t.get("config") != config or t.get("batch") != batch:
+        return None
+    return t
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_cpus():
+    """(CPUs in sched_getaffinity, cgroup CPU quota in whole CPUs or None).  On the GPU box the
+    affinity mask names every core of the host while the job's cgroup grants a share of them
+    (cpu.max): running one OpenMP thread per affinity core there oversubscribes the quota."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != "max":
+                quota = max(1, int(float(q) / float(per)))
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, q // per)
+        except (OSError, ValueError):
+            pass
+    return affinity, quota
+
+
 def cpu_baseline(p, batch, budget_s=12.0):
-    """The oracle (C restatement of the reference path, OpenMP over the batch) on the host."""
+    """The oracle (C restatement of the reference path, OpenMP over the batch) on ALL the host
+    cores this process may run on, plus a 1-thread run beside it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # CPU baseline leg only
 
-    threads = max(1, min(16, os.cpu_count() or 1))
-    n0 = min(256, batch["x0"].shape[0])
+    affinity, quota = host_cpus()
+    threads = max(1, min(affinity, quota or affinity))
+    n0 = min(max(256, 4 * threads), batch["x0"].shape[0])
     sub = {k: v[:n0] for k, v in batch.items()}
     t = time.perf_counter()
     oracle.srbm_batch(p, sub["x0"], sub["xref"], sub["lin"], sub["contact"], nthreads=threads)
     rate0 = n0 / max(1e-6, time.perf_counter() - t)
-    n = int(min(batch["x0"].shape[0], max(n0, rate0 * budget_s)))
+    n = int(min(batch["x0"].shape[0], max(n0, rate0 * budget_s / 2)))
     sub = {k: v[:n] for k, v in batch.items()}
     # repeat the sample until ~budget_s of CPU work is timed (10-30 s guideline)
-    o, done, dt, passes = None, 0, 0.0, 0
+    done, dt, passes = 0, 0.0, 0
     while passes == 0 or (dt < budget_s and passes < 8):
         t = time.perf_counter()
-        r = oracle.srbm_batch(p, sub["x0"], sub["xref"], sub["lin"], sub["contact"],
-                              nthreads=threads)
+        oracle.srbm_batch(p, sub["x0"], sub["xref"], sub["lin"], sub["contact"], nthreads=threads)
         dt += time.perf_counter() - t
         done += n
         passes += 1
-        o = o if o is not None else r
     n1 = min(n, max(16, int(done / dt / threads * 2.0)))  # ~2 s single-thread sample
     t = time.perf_counter()
     oracle.srbm_batch(p, sub["x0"][:n1], sub["xref"][:n1], sub["lin"][:n1], sub["contact"][:n1],
                       nthreads=1)
     one = n1 / (time.perf_counter() - t)
     return dict(value=done / dt, unit="QP/s", cores=threads, kind="port",
-                single_thread_value=one,
-                sample=f"first {n} instances of the rank-0 batch x {passes} passes, "
+                nproc=os.cpu_count(), affinity_cpus=affinity, cgroup_cpu_quota=quota,
+                cpu_model=cpu_model(), single_thread_value=one,
+                sample=f"first {n} instances of the rank-0 shard x {passes} passes, "
                        f"oracle/mpcqp_oracle.c (reference-literal dense condensing + "
-                       f"Goldfarb-Idnani), OpenMP {threads} threads, {dt:.1f} s"), o
+                       f"Goldfarb-Idnani), OpenMP {threads} threads = every CPU the job may "
+                       f"use (min of sched_getaffinity {affinity} and the cgroup quota "
+                       f"{quota}), {dt:.1f} s; 1 thread: {n1} instances")
 
 
 def host_staged_rate(eng, batch, p, reps=5):
@@ -127,8 +200,8 @@ def gait_fused_rate(eng, p, B, seed, reps=10):
     import mpcqp
     if not eng.fast_path or p["model"] != 0:
         return None
-    Cc = 16
-    g = eng.upload_gait(mpcqp.make_gait_states(p, B // Cc, seed=seed, candidates=Cc))
+    g = eng.upload_gait(mpcqp.make_gait_states(p, B // CANDIDATES, seed=seed,
+                                               candidates=CANDIDATES))
     eng.solve_gait(g)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -140,121 +213,324 @@ def gait_fused_rate(eng, p, B, seed, reps=10):
     return g["B"] * reps / (e0.elapsed_time(e1) * 1e-3)
 
 
+def time_config(config, B, seed, steps=10, warmup=2, gait=None, device=0):
+    """One single-GPU config: fused-kernel ms (HIP events on the engine's stream), QP/s, mean
+    solver iterations, solved fraction and the SURVEY 8d algorithmic-flop fraction."""
+    import torch
+
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+
+    p = mpcqp.model_params(config)
+    batch = mpcqp.make_batch(p, B, seed=seed, gait=gait) if gait else \
+        mpcqp.make_batch(p, B, seed=seed)
+    eng = BatchEngine(p, device=device)
+    d = eng.upload(batch)
+    for _ in range(warmup):
+        eng.solve(d)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    for e0, e1 in ev:
+        e0.record(stream)
+        eng.solve(d)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    st = d["status"].cpu().numpy()
+    it = d["iters"].cpu().numpy()
+    f_qp = flops_per_qp(p, it.mean())
+    ach = f_qp * B / (ms * 1e-3) / 1e12
+    out = dict(batch=B, nx=p["nx"], nu=p["nu"], N=p["N"],
+               constraints="box+friction" if p["constraints"] else "box",
+               gait=gait or "alternating (calculateGait, swing = stance = 0.5 s)",
+               R=float(p["R"][0, 0]), kernel=eng.fused_kernel, kernel_ms=ms,
+               qps=B / (ms * 1e-3), mean_solver_iters=float(it.mean()),
+               max_solver_iters=int(it.max()), solved_frac=float(np.mean(st == 0)),
+               algorithmic_flops_per_qp=f_qp, achieved_tflops=ach,
+               frac=ach / FP64_PEAK_TFLOPS)
+    eng.close()
+    return out
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv):
+    """Start N ranks as children (torch.distributed.run) and exit with their status.  The
+    parent never touches the GPU (no exec from a GPU-initialised process)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def shard(total_states, world, rank):
+    """contiguous range of whole states for `rank` -> (first state, number of states)"""
+    base, rem = divmod(total_states, world)
+    s0 = rank * base + min(rank, rem)
+    return s0, base + (1 if rank < rem else 0)
+
+
+def slice_batch(batch, i0, n):
+    return {k: np.ascontiguousarray(v[i0:i0 + n]) for k, v in batch.items()}
+
+
+def synthetic_shard(B, nV, seed, rank, index_base):
+    """--selection-dry-run: seeded cost/status/U of a shard (a function of the global index,
+    so the global argmin does not depend on how the batch is split)"""
+    gi = index_base + np.arange(B)
+    rng = np.random.default_rng([seed] + [int(x) for x in gi[:1]])
+    cost = np.cos(gi * 0.7071 + seed) * 1e3 + np.sin(gi * 1.3) * 10.0
+    status = np.where((gi % 7) == 3, 3, 0).astype(np.int32)
+    U = (gi[:, None] * 1e-3 + np.arange(nV)[None, :]).astype(np.float64)
+    del rng
+    return cost, status, U
+
+
 def main():
+    argv = sys.argv[1:]
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=65536, help="instances per GPU")
+    ap.add_argument("--global-batch", type=int, default=65536,
+                    help="instances over all GPUs (strong scaling: split over the ranks)")
+    ap.add_argument("--weak-batch", type=int, default=65536,
+                    help="instances per GPU of the weak-scaling (config D) line; 0 = skip")
     ap.add_argument("--config", default="B")
     ap.add_argument("--seed", type=int, default=20250404)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-per-config", action="store_true")
+    ap.add_argument("--selection-dry-run", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, argv))
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
 
     import torch
     import torch.distributed as dist
 
     import mpcqp
-    from mpcqp.dist import select_global
-    from mpcqp.engine import BatchEngine
+    from mpcqp.dist import decode_record, host_record, host_reduce_records, select_global
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dry = args.selection_dry_run
+    if dry:
+        dev = torch.device("cpu")
+        if world > 1:
+            dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device(f"cuda:{local}")
+        if world > 1:
+            dist.init_process_group("nccl", device_id=dev)
 
     p = mpcqp.model_params(args.config)
-    B = args.batch
-    batch = mpcqp.make_batch(p, B, seed=args.seed + rank)
-    eng = BatchEngine(p, device=local)
-    d = eng.upload(batch)
-    nV = eng.nV
-    ubest = torch.zeros(nV, dtype=torch.float64, device=f"cuda:{local}")
+    nV = p["nu"] * p["N"]
+    G = args.global_batch
+    S_total = G // CANDIDATES
+    if S_total * CANDIDATES != G or S_total < world:
+        raise SystemExit(f"--global-batch must be a multiple of {CANDIDATES} with >= 1 state "
+                         "per rank")
+    s0, ns = shard(S_total, world, rank)
+    i0, B = s0 * CANDIDATES, ns * CANDIDATES
 
-    def step():
-        eng.solve(d)
-        key = eng.select_min(d, index_base=rank * B)
-        if world > 1:
-            select_global(dist, key, d["U"], B, ubest)
+    def run_line(batch_local, index_base, steps, warmup):
+        """time `steps` steps of solve + selection on this rank's shard; returns
+        (elapsed max over ranks, kernel ms, select ms, best record, status, iters, eng)"""
+        Bl = batch_local["x0"].shape[0] if not dry else batch_local["B"]
+        rec = torch.zeros(1 + nV, dtype=torch.int64, device=dev)
+        gathered = torch.zeros((world, 1 + nV), dtype=torch.int64, device=dev)
+        best = torch.zeros(1 + nV, dtype=torch.int64, device=dev)
+        if dry:
+            cost, status, U = batch_local["cost"], batch_local["status"], batch_local["U"]
+            eng = None
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for s in range(args.steps):
-        e = ev[s]
-        e[0].record(stream)
-        eng.solve(d)
-        e[1].record(stream)
-        e[2].record(stream)
-        key = eng.select_min(d, index_base=rank * B)
-        e[3].record(stream)
+            def step():
+                rec.copy_(torch.from_numpy(host_record(cost, status, U, index_base)))
+                if world > 1:
+                    select_global(dist, rec, gathered, best, host_reduce_records)
+                else:
+                    best.copy_(rec)
+        else:
+            from mpcqp.engine import BatchEngine
+            eng = BatchEngine(p, device=local)
+            d = eng.upload(batch_local)
+
+            def step():
+                eng.solve(d)
+                eng.select_record(d, rec, index_base=index_base)
+                if world > 1:
+                    select_global(dist, rec, gathered, best, eng.reduce_records)
+                else:
+                    best.copy_(rec)
+
+        def sync():
+            if not dry:
+                torch.cuda.synchronize()
+
+        for _ in range(warmup):
+            step()
+        sync()
         if world > 1:
-            select_global(dist, key, d["U"], B, ubest)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    mpc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
-    sel_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))
-    status = d["status"].cpu().numpy()
-    iters = d["iters"].cpu().numpy()
-    solved = float(np.mean(status == 0))
+            dist.barrier()
+        sync()
+        evs = None
+        if not dry:
+            stream = torch.cuda.current_stream()
+            evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+        t0 = time.perf_counter()
+        for s in range(steps):
+            if dry:
+                step()
+                continue
+            e = evs[s]
+            e[0].record(stream)
+            eng.solve(d)
+            e[1].record(stream)
+            e[2].record(stream)
+            eng.select_record(d, rec, index_base=index_base)
+            e[3].record(stream)
+            if world > 1:
+                select_global(dist, rec, gathered, best, eng.reduce_records)
+            else:
+                best.copy_(rec)
+        sync()
+        if world > 1:
+            dist.barrier()
+        sync()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        mpc_ms = sel_ms = None
+        if not dry:
+            mpc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+            sel_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
+            status = d["status"].cpu().numpy()
+            iters = d["iters"].cpu().numpy()
+        else:
+            status, iters = batch_local["status"], np.zeros(Bl, np.int32)
+        return elapsed, mpc_ms, sel_ms, best.cpu().numpy(), status, iters, eng, \
+            (batch_local if dry else None)
+
+    # ---- strong scaling: the global batch split over the ranks (the metric) ----------------
+    if dry:
+        cost, status, U = synthetic_shard(B, nV, args.seed, rank, i0)
+        local_batch = dict(B=B, cost=cost, status=status, U=U)
+    else:
+        full = mpcqp.make_batch(p, G, seed=args.seed)
+        local_batch = slice_batch(full, i0, B)
+        del full
+    elapsed, mpc_ms, sel_ms, best, status, iters, eng, _ = run_line(
+        local_batch, i0, args.steps, args.warmup)
+    bcost, bidx, bU = decode_record(best)
+
+    # ---- weak scaling (config D at N = 8): 65,536 per GPU, independent shards -------------
+    weak = None
+    if args.weak_batch and world > 1 and not dry:
+        Bw = args.weak_batch
+        wb = mpcqp.make_batch(p, Bw, seed=args.seed + 1000 + rank)
+        el_w, ms_w, _, best_w, st_w, _, eng_w, _ = run_line(wb, rank * Bw, args.steps,
+                                                            args.warmup)
+        eng_w.close()
+        cw, iw, _ = decode_record(best_w)
+        weak = dict(batch_per_gpu=Bw, global_batch=Bw * world, value=Bw * world /
+                    (el_w / args.steps), ms_per_step=el_w / args.steps * 1e3,
+                    kernel_ms=ms_w, solved_frac_rank0=float(np.mean(st_w == 0)),
+                    selected=dict(index=iw, cost=cw), scaling="weak",
+                    note="config D at N = 8 (524,288 instances); shards seeded per rank")
 
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
-        total = B * world
-        fl = algorithmic_flops(p["nx"], p["nu"], p["N"])
-        f_qp = fl["condense"] + fl["solve_fixed"] + fl["per_iter"] * float(iters.mean())
-        dom_flops = f_qp * B
-        achieved = dom_flops / (mpc_ms * 1e-3) / 1e12
-        traffic, traffic_tag = pmc_traffic(args.config, B)
-        out = dict(
-            metric="QP solves/sec, 13-state N=10 SRBM MPC, batch=65536 at 1/2/4/8 MI355X",
-            value=total / (elapsed / args.steps), unit="QP/s", n_gpus=world, steps=args.steps,
-            warmup=args.warmup, ms_per_step=ms_per_step, higher_is_better=True,
-            scaling="weak", vs_baseline=None, dtype="f64",
-            data="synthetic (seeded SURVEY.md 8d TRON1 states x 16 gait candidates)",
-            config=dict(workload=f"TRON1 SRBM MPC {p['nx']}x{p['nu']} N={p['N']} "
-                                 f"({'box+friction' if p['constraints'] else 'box'}), "
-                                 f"linearise+discretise+condense+solve, batch {B} per GPU",
-                        batch_per_gpu=B, global_batch=total, horizon=p["N"], nx=p["nx"],
-                        nu=p["nu"], config=args.config, parallelism=f"dp{world}",
-                        solved_frac=solved, mean_solver_iters=float(iters.mean()),
-                        fast_path=eng.fast_path,
-                        kernel_ms={eng.fused_kernel: mpc_ms, "k_select_min": sel_ms}),
-            roofline=dict(bound="mfma", kernel=eng.fused_kernel, achieved=achieved,
-                          peak=FP64_PEAK_TFLOPS, unit="TFLOP/s",
-                          frac=achieved / FP64_PEAK_TFLOPS, traffic=traffic,
-                          traffic_source=(f"profiles/{traffic_tag}_summary.json (rocprofv3 PMC, "
-                                          "2 x FETCH_SIZE + WRITE_SIZE)") if traffic else None,
-                          algorithmic_bytes_per_launch=algorithmic_bytes(
-                              p["nx"], p["nu"], p["N"]) * B,
-                          algorithmic_flops_per_qp=f_qp,
-                          basis="SURVEY.md 8d algorithmic flops (F_fixed + F_iter x mean iters); "
-                                "the closed-form path executes fewer, so frac can exceed 1",
-                          whole_step_tflops=dom_flops / (ms_per_step * 1e-3) / 1e12),
-        )
-        out["config"]["pcie_inclusive_qps"] = host_staged_rate(eng, batch, p)
-        out["config"]["gait_fused_qps"] = gait_fused_rate(eng, p, B, args.seed)
-        if not args.no_cpu_baseline:
-            cb, _ = cpu_baseline(p, batch)
-            out["cpu_baseline"] = cb
+        value = G / (elapsed / args.steps)
+        solved = float(np.mean(status == 0))
+        out = dict(metric=METRIC, value=value, unit="QP/s", n_gpus=world, steps=args.steps,
+                   warmup=args.warmup, ms_per_step=ms_per_step, higher_is_better=True,
+                   scaling="strong", vs_baseline=None, dtype="f64",
+                   data="synthetic (seeded SURVEY.md 8d TRON1 states x 16 gait candidates)")
+        cfg = dict(workload=f"TRON1 SRBM MPC {p['nx']}x{p['nu']} N={p['N']} "
+                            f"({'box+friction' if p['constraints'] else 'box'}, R = "
+                            f"{p['R'][0, 0]:g} I), linearise+discretise+condense+solve + "
+                            f"min-cost selection, global batch {G} split over {world} GPU(s)",
+                   global_batch=G, batch_per_gpu=B, horizon=p["N"], nx=p["nx"], nu=p["nu"],
+                   config=args.config, parallelism=f"dp{world}",
+                   selection="one all-gather of [key | U] records + k_reduce_records"
+                             if world > 1 else "k_select_min record (single GPU)",
+                   selected=dict(index=bidx, cost=bcost))
+    if rank == 0 and dry:
+        cfg["dry_run"] = "selection only: synthetic costs, gloo, no solve"
+        out["config"] = cfg
         print(json.dumps(out), flush=True)
-    eng.close()
+    elif rank == 0:
+        f_qp = flops_per_qp(p, iters.mean())
+        achieved = f_qp * B / (mpc_ms * 1e-3) / 1e12
+        traffic, traffic_tag = pmc_traffic(args.config, B)
+        cfg.update(solved_frac=solved, mean_solver_iters=float(iters.mean()),
+                   fast_path=eng.fast_path,
+                   kernel_ms={eng.fused_kernel: mpc_ms, "k_select_min": sel_ms})
+        roof = dict(bound="mfma", compute_unit="fp64 VALU (k_mpc_pair issues no MFMA)",
+                    kernel=eng.fused_kernel, achieved=achieved, peak=FP64_PEAK_TFLOPS,
+                    unit="TFLOP/s", frac=achieved / FP64_PEAK_TFLOPS, traffic=traffic,
+                    traffic_source=(f"profiles/{traffic_tag}_summary.json (rocprofv3 PMC, "
+                                    "2 x FETCH_SIZE + WRITE_SIZE)") if traffic else None,
+                    algorithmic_bytes_per_launch=algorithmic_bytes(p["nx"], p["nu"], p["N"]) * B,
+                    algorithmic_flops_per_qp=f_qp,
+                    basis="SURVEY.md 8d algorithmic flops (F_fixed + F_iter x mean iters) per "
+                          "QP x batch / fused-kernel time; the closed-form path executes "
+                          "fewer, so frac is a work rate, not pipe utilisation (see "
+                          "executed_tflops / pipe_frac)",
+                    whole_step_tflops=f_qp * B / (ms_per_step * 1e-3) / 1e12)
+        ex = pmc_executed(args.config, B)
+        if ex:
+            per_launch = ex["executed_flops_per_launch"]
+            roof["executed_tflops"] = per_launch / (mpc_ms * 1e-3) / 1e12
+            roof["pipe_frac"] = roof["executed_tflops"] / FP64_PEAK_TFLOPS
+            roof["executed_source"] = f"profiles/{ex.get('file', 'pmc_flops.json')} " \
+                                      "(SQ_INSTS_VALU_{FMA,MUL,ADD}_F64 x 64 lanes)"
+        out["roofline"] = roof
+        if weak:
+            cfg["weak"] = weak
+        if world == 1:
+            cfg["pcie_inclusive_qps"] = host_staged_rate(eng, local_batch, p)
+            cfg["gait_fused_qps"] = gait_fused_rate(eng, p, B, args.seed)
+        out["config"] = cfg
+        eng.close()
+        if world == 1 and not args.no_per_config:
+            per = {}
+            for name, conf, Bc, gait in (("B@4096", "B", 4096, None),
+                                         ("C@65536", "C", 65536, None),
+                                         ("L@65536", "L", 65536, None),
+                                         ("B-standing@65536", "B", 65536, "standing"),
+                                         ("C-mixed@65536", "C", 65536, "mixed")):
+                try:
+                    per[name] = time_config(conf, Bc, args.seed, gait=gait)
+                except Exception as exc:  # report, never hide
+                    per[name] = dict(error=f"{type(exc).__name__}: {exc}")
+            cfg["per_config"] = per
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(p, local_batch)
+        print(json.dumps(out), flush=True)
+    elif eng is not None:
+        eng.close()
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -34,6 +34,9 @@
  * mpcqp_batch_condense_solve      QPSolver::buildQPParams + QPSolver::solveQP, batched, fused
  *                                 (H never leaves the chip)
  * mpcqp_batch_select_min          (new) per-rank min-cost key for the multi-GPU selection
+ * mpcqp_batch_select_record       (new) per-rank selection record [key | winner's U] for the
+ *                                 one-collective multi-GPU selection
+ * mpcqp_reduce_records            (new) global winner from the all-gathered records
  * mpcqp_batch_solve_gait          mpcQP::mpcQP xref (include/mpcQP.h:74-97) + MPC::calculateGait
  *                                 (include/MPCController.h:61-75) on device, then the fused step
  * mpcqp_batch_select_state        (new) best gait candidate per state
@@ -185,6 +188,16 @@ int mpcqp_batch_solve_host(mpcqp_ctx *ctx, int B, const double *x0, const double
  * (the same stream, or a synchronisation after mpcqp_set_stream). */
 int mpcqp_batch_select_min(mpcqp_ctx *ctx, int B, const double *cost, const int *status,
                            int64_t index_base, int64_t *key);
+/* Selection record for the multi-GPU path: record [1 + nu*N] int64 (device) receives the
+ * key of mpcqp_batch_select_min in record[0] and the winning instance's U row (nu*N doubles,
+ * bit copies) in record[1..]; all zeros after the key 0x7fffffffffffffff when no instance is
+ * valid.  Same launch and ordering rules as mpcqp_batch_select_min; index_base + B must fit
+ * in 31 bits.  The ranks exchange records with ONE all-gather (RCCL), then each rank runs
+ * mpcqp_reduce_records(ctx, n_ranks, gathered [n][1 + nu*N], best [1 + nu*N]) to pick the
+ * minimum key's record on device: no host synchronisation, no second collective. */
+int mpcqp_batch_select_record(mpcqp_ctx *ctx, int B, const double *cost, const int *status,
+                              const double *U, int64_t index_base, int64_t *record);
+int mpcqp_reduce_records(mpcqp_ctx *ctx, int n, const int64_t *records, int64_t *best);
 
 /* ---- device-generated inputs, per-state selection and the closed loop ---- *
  * SRBM fast-path contexts only.  S states x C gait candidates, instance b = s*C + c.

@@ -168,9 +168,11 @@ constexpr int kSelPerBlock = 1024;
 __global__ void __launch_bounds__(256) k_select_min(int B, const double *cost, const int *status,
                                                      long long base, unsigned long long *key,
                                                      unsigned long long *partial,
-                                                     unsigned int *ticket) {
+                                                     unsigned int *ticket, const double *U,
+                                                     int nV, double *rec_u) {
     __shared__ unsigned long long red[4];
     __shared__ bool last;
+    __shared__ unsigned long long win;
     unsigned long long best = 0x7fffffffffffffffull;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B; i += gridDim.x * blockDim.x) {
         if (status[i] != 0) continue;
@@ -213,8 +215,42 @@ __global__ void __launch_bounds__(256) k_select_min(int B, const double *cost, c
         unsigned long long m = red[0];
         for (int w = 1; w < (int)(blockDim.x >> 6); ++w) m = red[w] < m ? red[w] : m;
         *key = m;
+        win = m;
         __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (!rec_u) return;
+    // selection record: the winner's U row after the key (zeros when no instance is valid)
+    __syncthreads();
+    const unsigned long long m = win;
+    const bool none = m == 0x7fffffffffffffffull;
+    const long long li = none ? 0 : (long long)(m & 0x7fffffffull) - (base & 0x7fffffffll);
+    for (int e = threadIdx.x; e < nV; e += blockDim.x)
+        rec_u[e] = none ? 0.0 : U[(size_t)li * nV + e];
+}
+
+// Global selection over n gathered records [key | U(nV)] (one per rank, after one all-gather):
+// the minimum key's record is copied to `best`.  Keys carry the global index, so they are
+// distinct unless invalid (0x7fff...); an all-invalid set yields that key and the first
+// record's U, which is all zeros by construction of k_select_min.
+__global__ void __launch_bounds__(64) k_reduce_records(int n, int nV, const long long *rec,
+                                                       long long *best) {
+    __shared__ int who;
+    unsigned long long k = 0x7fffffffffffffffull;
+    int idx = 0;
+    for (int r = threadIdx.x; r < n; r += 64) {
+        const unsigned long long v = (unsigned long long)rec[(size_t)r * (nV + 1)];
+        if (v < k) { k = v; idx = r; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long t = __shfl_xor(k, o, 64);
+        const int ti = __shfl_xor(idx, o, 64);
+        if (t < k || (t == k && ti < idx)) { k = t; idx = ti; }
+    }
+    if (threadIdx.x == 0) who = idx;
+    __syncthreads();
+    const long long *src = rec + (size_t)who * (nV + 1);
+    for (int e = threadIdx.x; e <= nV; e += 64) best[e] = src[e];
 }
 
 __global__ void __launch_bounds__(64) k_plant(int nx, int nu, const double *Ad, const double *Bd,
@@ -1249,7 +1285,32 @@ int mpcqp_batch_select_min(mpcqp_ctx *c, int B, const double *cost, const int *s
     const int blocks = std::max(1, std::min(kSelMaxBlocks, (B + kSelPerBlock - 1) / kSelPerBlock));
     hipLaunchKernelGGL(k_select_min, dim3(blocks), dim3(256), 0, c->stream, B, cost, status,
                        (long long)index_base, k, c->dsel,
-                       reinterpret_cast<unsigned int *>(c->dsel + kSelMaxBlocks));
+                       reinterpret_cast<unsigned int *>(c->dsel + kSelMaxBlocks),
+                       (const double *)nullptr, 0, (double *)nullptr);
+    return hip_status(hipGetLastError());
+}
+
+int mpcqp_batch_select_record(mpcqp_ctx *c, int B, const double *cost, const int *status,
+                              const double *U, int64_t index_base, int64_t *record) {
+    if (!c || !record || B < 0 || (B > 0 && (!cost || !status || !U))) return MPCQP_ERR_BAD_ARG;
+    if (index_base < 0 || index_base + (int64_t)B > 0x7fffffffll) return MPCQP_ERR_BAD_DIMS;
+    hipSetDevice(c->device);
+    unsigned long long *k = reinterpret_cast<unsigned long long *>(record);
+    const int nV = c->m.nu * c->m.N;
+    const int blocks = std::max(1, std::min(kSelMaxBlocks, (B + kSelPerBlock - 1) / kSelPerBlock));
+    hipLaunchKernelGGL(k_select_min, dim3(blocks), dim3(256), 0, c->stream, B, cost, status,
+                       (long long)index_base, k, c->dsel,
+                       reinterpret_cast<unsigned int *>(c->dsel + kSelMaxBlocks), U, nV,
+                       reinterpret_cast<double *>(record + 1));
+    return hip_status(hipGetLastError());
+}
+
+int mpcqp_reduce_records(mpcqp_ctx *c, int n, const int64_t *records, int64_t *best) {
+    if (!c || !records || !best || n <= 0) return MPCQP_ERR_BAD_ARG;
+    hipSetDevice(c->device);
+    hipLaunchKernelGGL(k_reduce_records, dim3(1), dim3(64), 0, c->stream, n, c->m.nu * c->m.N,
+                       reinterpret_cast<const long long *>(records),
+                       reinterpret_cast<long long *>(best));
     return hip_status(hipGetLastError());
 }
 

@@ -26,7 +26,8 @@ EXPORTS = [
     "mpcqp_batch_condense", "mpcqp_batch_solve_qp", "mpcqp_batch_solve",
     "mpcqp_ctx_fast_path", "mpcqp_batch_discretize", "mpcqp_batch_condense_solve",
     "mpcqp_debug_phase_cycles", "mpcqp_batch_solve_host",
-    "mpcqp_batch_select_min", "mpcqp_enable_timing", "mpcqp_last_kernel_ms",
+    "mpcqp_batch_select_min", "mpcqp_batch_select_record", "mpcqp_reduce_records",
+    "mpcqp_enable_timing", "mpcqp_last_kernel_ms",
     "mpcqp_batch_solve_gait", "mpcqp_batch_select_state", "mpcqp_batch_plant_srbm",
     "mpcqp_rollout", "mpcqp_fk_feet", "mpcqp_kf_update",
     "mpcqp_status_string", "mpcqp_device_count",
@@ -81,6 +82,8 @@ def lib():
     L.mpcqp_batch_discretize.argtypes = [vp, i, vp, vp]
     L.mpcqp_batch_condense_solve.argtypes = [vp, i] + [vp] * 8
     L.mpcqp_batch_select_min.argtypes = [vp, i, vp, vp, C.c_int64, vp]
+    L.mpcqp_batch_select_record.argtypes = [vp, i, vp, vp, vp, C.c_int64, vp]
+    L.mpcqp_reduce_records.argtypes = [vp, i, vp, vp]
     L.mpcqp_batch_solve_gait.argtypes = [vp, i, i] + [vp] * 4 + [C.c_float, C.c_float] + [vp] * 4
     L.mpcqp_batch_select_state.argtypes = [vp, i, i] + [vp] * 6
     L.mpcqp_batch_plant_srbm.argtypes = [vp, i, i] + [vp] * 5

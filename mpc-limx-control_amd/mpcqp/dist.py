@@ -1,14 +1,18 @@
 """Multi-GPU min-cost selection.
 
 The batch of (state, gait-candidate) QPs is sharded in contiguous ranges over the ranks (one
-process per GPU); the solves need no communication.  The only exchange is the selection of the
-global minimum-cost candidate: every rank reduces its shard to one 8-byte key on device
-(mpcqp_batch_select_min), ONE MIN all-reduce (RCCL over xGMI for backend "nccl", gloo on CPU)
-finds the global key, and the owning rank broadcasts its U row (nu*N doubles).
+process per GPU, ranges aligned to whole states); the solves need no communication.  The only
+exchange is the selection of the global minimum-cost candidate, in ONE collective:
 
-key = (order-preserving bits of float32(cost)) << 31 | global index  -- non-negative int64, so
-a signed MIN is the lexicographic (cost, index) minimum: ties go to the lowest index, as in the
-host reference (encode_key).
+  1. each rank reduces its shard on device to a record [key | winner's U]
+     (mpcqp_batch_select_record: key = order-preserving bits of float32(cost) << 31 | global
+     index; U row nu*N doubles; an all-invalid shard gives key INT64_MAX and U = 0),
+  2. one all-gather of the records (RCCL over xGMI for backend "nccl", gloo on CPU),
+  3. every rank picks the minimum key's record on device (mpcqp_reduce_records).
+
+No `.item()`, no host synchronisation and no owner broadcast inside the step.  Keys are
+non-negative int64, so the minimum is the lexicographic (fp32 cost, global index) minimum:
+ties go to the lowest index, as in the host reference (host_select).
 """
 from __future__ import annotations
 
@@ -16,23 +20,57 @@ import numpy as np
 
 from .engine import decode_key, encode_key
 
+NO_KEY = 0x7FFFFFFFFFFFFFFF
 
-def select_global(dist, key_tensor, U_local, per_rank: int, ubest):
-    """All-reduce the local key (int64 tensor of shape [1]) with MIN, then broadcast the
-    winner's U row into `ubest` on every rank.  Shards are equal (`per_rank` instances, rank r
-    owns global indices [r*per_rank, (r+1)*per_rank)).  Returns (cost_f32, global_index)."""
-    dist.all_reduce(key_tensor, op=dist.ReduceOp.MIN)
-    cost, gidx = decode_key(int(key_tensor.item()))
-    owner = gidx // per_rank
-    if owner == dist.get_rank():
-        ubest.copy_(U_local[gidx - owner * per_rank])
-    dist.broadcast(ubest, src=owner)
-    return cost, gidx
+
+def select_global(dist, record, gathered, best, reduce):
+    """record: int64 [1 + nV] of this rank; gathered: int64 [world, 1 + nV] buffer; best:
+    int64 [1 + nV] output (same on every rank); reduce(gathered, best): the device (or host)
+    record reduction.  One collective."""
+    dist.all_gather_into_tensor(gathered.view(-1), record)
+    reduce(gathered, best)
+    return best
+
+
+def decode_record(best) -> tuple:
+    """(float32 cost or inf, global index or -1, U row float64) from a selection record"""
+    b = np.asarray(best, dtype=np.int64)
+    key = int(b[0])
+    U = b[1:].view(np.float64).copy()
+    if key == NO_KEY:
+        return float("inf"), -1, U
+    c, i = decode_key(key)
+    return c, i, U
+
+
+def host_record(costs, status, U, index_base: int = 0):
+    """host restatement of mpcqp_batch_select_record over one shard"""
+    U = np.asarray(U, dtype=np.float64)
+    nV = U.shape[1] if U.ndim == 2 else 0
+    rec = np.zeros(1 + nV, dtype=np.int64)
+    key = host_keys(costs, status, index_base)
+    rec[0] = key
+    if key != NO_KEY:
+        li = (key & 0x7FFFFFFF) - index_base
+        rec[1:] = U[li].view(np.int64)
+    return rec
+
+
+def host_reduce_records(gathered, best):
+    """host restatement of mpcqp_reduce_records (numpy or CPU torch int64 arrays)"""
+    g = gathered.numpy() if hasattr(gathered, "numpy") else np.asarray(gathered)
+    j = int(np.argmin(g[:, 0].astype(np.uint64)))
+    if hasattr(best, "copy_"):
+        import torch
+        best.copy_(torch.from_numpy(g[j].copy()))
+    else:
+        best[...] = g[j]
+    return best
 
 
 def host_keys(costs, status, index_base: int = 0):
     """host restatement of k_select_min over one shard (min key, INT64_MAX if none valid)"""
-    best = 0x7FFFFFFFFFFFFFFF
+    best = NO_KEY
     for i, (c, s) in enumerate(zip(costs, status)):
         if s == 0:
             best = min(best, encode_key(float(c), index_base + i))
@@ -40,9 +78,12 @@ def host_keys(costs, status, index_base: int = 0):
 
 
 def host_select(costs, status):
-    """reference: global (float32 cost, lowest index) minimum over valid instances"""
+    """reference: global (float32 cost, lowest index) minimum over valid instances
+    ((inf, -1) if none is valid)"""
     c = np.asarray(costs, dtype=np.float64).astype(np.float32)
     ok = np.asarray(status) == 0
     idx = np.nonzero(ok)[0]
+    if idx.size == 0:
+        return float("inf"), -1
     j = idx[np.lexsort((idx, c[idx]))[0]]
     return float(c[j]), int(j)

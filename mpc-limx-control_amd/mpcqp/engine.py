@@ -169,6 +169,19 @@ class BatchEngine:
             _ptr(d["key"])))
         return d["key"]
 
+    def select_record(self, d, rec, index_base: int = 0):
+        """rec: int64 device tensor [1 + nV] <- [min key | winner's U bits] of this shard"""
+        check("mpcqp_batch_select_record", lib().mpcqp_batch_select_record(
+            self.ctx, d["B"], _ptr(d["cost"]), _ptr(d["status"]), _ptr(d["U"]), int(index_base),
+            _ptr(rec)))
+        return rec
+
+    def reduce_records(self, gathered, best):
+        """gathered: int64 [n, 1 + nV] (one record per rank) -> best [1 + nV], on device"""
+        check("mpcqp_reduce_records", lib().mpcqp_reduce_records(
+            self.ctx, int(gathered.shape[0]), _ptr(gathered), _ptr(best)))
+        return best
+
     def sync(self):
         check("mpcqp_sync", lib().mpcqp_sync(self.ctx))
 

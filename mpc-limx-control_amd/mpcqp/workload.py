@@ -29,8 +29,59 @@ def gait_contact_mask(N: int, Ts: float, phase0: float, swing=SWING_TIME, stance
     return mask
 
 
-def make_batch(p: dict, B: int, seed: int = DEFAULT_SEED, candidates: int = 16):
-    """-> dict(x0 [B,13], xref [B,N+1,13], lin [B,8], contact [B] uint64)"""
+def double_support_mask(N: int, Ts: float, phase0: float, duty: float = 0.6,
+                        cycle: float = 1.0) -> int:
+    """Walking gait with double-support phases (build-chosen; the reference's calculateGait
+    never puts both feet down): each foot is in contact for `duty` of the cycle, the right
+    foot half a cycle behind the left, so both are down for (2 duty - 1) of the cycle."""
+    mask = 0
+    for k in range(N):
+        t = phase0 + float(k) * Ts
+        if math.fmod(t, cycle) < duty * cycle:
+            mask |= 1 << (2 * k)
+        if math.fmod(t + 0.5 * cycle, cycle) < duty * cycle:
+            mask |= 1 << (2 * k + 1)
+    return mask
+
+
+def standing_mask(N: int) -> int:
+    """both feet in contact at every horizon step (a standing TRON1: nf = 6 N)"""
+    return (1 << (2 * N)) - 1
+
+
+GAITS = ("alternating", "standing", "double", "mixed")
+
+
+def contact_masks(gait: str, N: int, Ts: float, phase) -> np.ndarray:
+    """contact masks of a [S, C] array of candidate phases for one of GAITS:
+    alternating  MPC::calculateGait (include/MPCController.h:61-75), one stance foot per step
+    standing     both feet down (nf = 6 N)
+    double       double_support_mask (duty 0.6: 20 % of the cycle with both feet down)
+    mixed        per candidate c: alternating (c % 4 in {0, 1}), double (2) or standing (3)"""
+    S, C = phase.shape
+    out = np.zeros((S, C), dtype=np.uint64)
+    for s in range(S):
+        for c in range(C):
+            g = gait
+            if gait == "mixed":
+                g = ("alternating", "alternating", "double", "standing")[c % 4]
+            ph = float(phase[s, c])
+            if g == "alternating":
+                m = gait_contact_mask(N, Ts, ph)
+            elif g == "standing":
+                m = standing_mask(N)
+            elif g == "double":
+                m = double_support_mask(N, Ts, ph)
+            else:
+                raise ValueError(gait)
+            out[s, c] = m
+    return out
+
+
+def make_batch(p: dict, B: int, seed: int = DEFAULT_SEED, candidates: int = 16,
+               gait: str = "alternating"):
+    """-> dict(x0 [B,13], xref [B,N+1,13], lin [B,8], contact [B] uint64).  `gait` picks the
+    contact schedules of the candidates (GAITS); the default is the reference's calculateGait."""
     rng = np.random.default_rng(seed)
     N, nx, Ts = p["N"], p["nx"], p["Ts"]
     C = max(1, min(candidates, B))
@@ -72,8 +123,7 @@ def make_batch(p: dict, B: int, seed: int = DEFAULT_SEED, candidates: int = 16):
         lit = np.zeros((S, 8))
         lit[:, 0:3] = lin[:, 1:4]
         lin = lit
-    contact = np.array([[gait_contact_mask(N, Ts, float(phase[s, c])) for c in range(C)]
-                        for s in range(S)], dtype=np.uint64)
+    contact = contact_masks(gait, N, Ts, phase)
     rep = lambda a: np.repeat(a, C, axis=0)[:B]
     return dict(x0=np.ascontiguousarray(rep(x0)), xref=np.ascontiguousarray(rep(xref)),
                 lin=np.ascontiguousarray(rep(lin)), contact=np.ascontiguousarray(contact.reshape(-1)[:B]))

@@ -218,8 +218,9 @@ def test_full_size_metric_batch_properties(gpu, orc):
 
 def test_select_min_repeated_calls(gpu):
     """k_select_min reduces in one launch (last block re-arms the context's ticket): repeated
-    calls on one context with different batch sizes (1 .. 1024 blocks, B = 0), index bases and
-    failed instances each return the host key"""
+    calls on one context with different batch sizes (1 block up to the 1024-block clamp with a
+    grid-stride loop: 1,100,000 instances; B = 0), index bases and failed instances each return
+    the host key"""
     import torch
     import mpcqp
     from mpcqp.engine import BatchEngine, encode_key
@@ -228,7 +229,7 @@ def test_select_min_repeated_calls(gpu):
     rng = np.random.default_rng(17)
     dev = torch.device("cuda:0")
     key = torch.zeros(1, dtype=torch.int64, device=dev)
-    for B in (0, 1, 255, 256, 257, 4096, 65536, 300000, 3):
+    for B in (0, 1, 255, 256, 257, 4096, 65536, 300000, 1_100_000, 3):
         cost = rng.normal(size=B) * 100.0
         status = np.where(rng.random(B) < 0.1, 3, 0).astype(np.int32)
         base = int(rng.integers(0, 1 << 20))
@@ -241,6 +242,57 @@ def test_select_min_repeated_calls(gpu):
         ok = np.nonzero(status == 0)[0]
         want = min((encode_key(cost[i], base + int(i)) for i in ok), default=0x7FFFFFFFFFFFFFFF)
         assert got == want, B
+    eng.close()
+
+
+def test_select_record_and_reduce(gpu):
+    """selection records (k_select_min with the winner's U row) and the device record
+    reduction of the one-collective multi-GPU selection: batch sizes through the
+    kSelMaxBlocks clamp and the grid-stride path (1,100,000 > 1024 x 1024), an all-invalid
+    shard (key INT64_MAX, U = 0), and the reduction over several ranks' records equal the
+    host restatements (mpcqp.dist.host_record / host_reduce_records)."""
+    import torch
+    import mpcqp
+    from mpcqp.dist import NO_KEY, host_record, host_reduce_records
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("B")
+    nV = p["nu"] * p["N"]
+    eng = BatchEngine(p)
+    rng = np.random.default_rng(29)
+    dev = torch.device("cuda:0")
+    recs = []
+    for r, B in enumerate((1, 4097, 1_100_000, 5, 300)):
+        cost = rng.normal(size=B) * 100.0
+        status = np.where(rng.random(B) < 0.2, 3, 0).astype(np.int32)
+        if r == 3:
+            status[:] = 2  # nothing valid on this shard
+        U = rng.normal(size=(B, nV))
+        base = r * 2_000_000
+        d = dict(B=B, cost=torch.tensor(cost, device=dev), status=torch.tensor(status, device=dev),
+                 U=torch.tensor(U, device=dev))
+        rec = torch.full((1 + nV,), -1, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        eng.select_record(d, rec, index_base=base)
+        eng.sync()
+        got = rec.cpu().numpy()
+        want = host_record(cost, status, U, base)
+        np.testing.assert_array_equal(got, want)
+        if r == 3:
+            assert got[0] == NO_KEY and not got[1:].any()
+        recs.append(want)
+    g = torch.tensor(np.stack(recs), device=dev)
+    best = torch.zeros(1 + nV, dtype=torch.int64, device=dev)
+    eng.reduce_records(g, best)
+    eng.sync()
+    ref = np.zeros(1 + nV, np.int64)
+    host_reduce_records(np.stack(recs), ref)
+    np.testing.assert_array_equal(best.cpu().numpy(), ref)
+    # all ranks invalid -> the no-selection record
+    g2 = torch.tensor(np.stack([recs[3], recs[3]]), device=dev)
+    eng.reduce_records(g2, best)
+    eng.sync()
+    b2 = best.cpu().numpy()
+    assert b2[0] == NO_KEY and not b2[1:].any()
     eng.close()
 
 

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Summarize a tools/pmc_flops.sh output directory into profiles/pmc_flops.json: executed FP64
+work of one kernel per launch (median over its dispatches).
+  executed_flops_per_launch  SQ_INSTS_VALU_FLOPS_FP64 (per-lane FLOPs of every FP64 VALU
+                             instruction, MFMA excluded) + 512 x SQ_INSTS_VALU_MFMA_MOPS_F64
+  lane_flops_upper_bound     64 x (2 FMA + MUL + ADD) F64 instructions (every lane counted)
+  mfma_busy_frac             SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)
+Usage: tools/summarize_flops.py PROFDIR TAG --kernel k_mpc_pair [--config B --batch 65536]"""
+import argparse
+import collections
+import csv
+import json
+import os
+import statistics as st
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_dispatch(path, kernel):
+    """{counter: median over dispatches of `kernel` of the per-dispatch total}"""
+    acc = collections.defaultdict(lambda: collections.defaultdict(float))
+    for r in csv.DictReader(open(path)):
+        if kernel not in r["Kernel_Name"]:
+            continue
+        acc[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    return {c: st.median(v.values()) for c, v in acc.items()}, \
+        {c: len(v) for c, v in acc.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("prof")
+    ap.add_argument("tag")
+    ap.add_argument("--kernel", default="k_mpc_pair")
+    ap.add_argument("--config", default="B")
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--out", default="pmc_flops.json")
+    a = ap.parse_args()
+    sq, n = per_dispatch(os.path.join(a.prof, "sq", "run_counter_collection.csv"), a.kernel)
+    try:
+        gr, _ = per_dispatch(os.path.join(a.prof, "grbm", "run_counter_collection.csv"), a.kernel)
+    except OSError:
+        gr = {}
+    g = lambda k: sq.get(k, 0.0)
+    executed = g("SQ_INSTS_VALU_FLOPS_FP64") + 512.0 * g("SQ_INSTS_VALU_MFMA_MOPS_F64")
+    upper = 64.0 * (2 * g("SQ_INSTS_VALU_FMA_F64") + g("SQ_INSTS_VALU_MUL_F64") +
+                    g("SQ_INSTS_VALU_ADD_F64"))
+    out = dict(tag=a.tag, kernel=a.kernel, config=a.config, batch=a.batch, file=a.out,
+               counters=sq, dispatches=n, grbm=gr,
+               executed_flops_per_launch=executed, lane_flops_upper_bound=upper,
+               mfma_flops_per_launch=512.0 * g("SQ_INSTS_VALU_MFMA_MOPS_F64"))
+    if gr.get("GRBM_GUI_ACTIVE"):
+        cyc = gr["GRBM_GUI_ACTIVE"] / 8.0  # summed over the 8 XCDs (MI355X_MICROARCH.md)
+        out["gui_active_cycles"] = cyc
+        out["mfma_busy_frac"] = g("SQ_VALU_MFMA_BUSY_CYCLES") / (cyc * 1024.0)
+    json.dump(out, open(os.path.join(ROOT, "profiles", a.out), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
