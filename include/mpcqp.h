@@ -74,7 +74,9 @@ extern "C" {
 #define MPCQP_MAX_NU 16
 #define MPCQP_MAX_N 32
 #define MPCQP_MAX_NV 256   /* NU*N */
-#define MPCQP_MAX_FREE 64  /* free (lb < ub) variables per solve */
+#define MPCQP_MAX_FREE 128 /* free (lb < ub) variables per solve: the batched fast path holds up
+                            * to 6N (every contact schedule); mpcqp_solve_dense and the generic
+                            * batched path hold 64 */
 
 /* layout flag of the dense constraint matrix handed to mpcqp_solve_dense */
 #define MPCQP_A_ROWMAJOR 0 /* qpOASES's convention (what QProblem::init expects)      */

@@ -23,10 +23,15 @@ struct FastKernels {
     const void *mpc_gen = nullptr;
     const void *pair = nullptr, *pair_gen = nullptr;  // two QPs per wave (nf <= 30)
     size_t pair_lds = 0;
+    const void *wg = nullptr;  // workgroup per QP for the overflow list (nf <= 6N)
+    size_t wg_lds = 0;
     const void *disc = nullptr, *cs = nullptr, *mpc = nullptr;
     size_t disc_lds = 0, cs_lds = 0, mpc_lds = 0;
     int nx = 0, nu = 0;
+    int prim_nf = 0;  // free variables the one-wave kernel holds (kPairCap or its NF)
 };
+
+constexpr int kPairCap = 30;  // free variables of one half of the paired kernel (mpc_pair.hpp)
 
 // per-family pickers (one translation unit each); false = not instantiated
 bool pick_fast_srbm10(bool fric, int nfmax, FastKernels &k);
@@ -34,6 +39,8 @@ bool pick_fast_srbm20(bool fric, int nfmax, FastKernels &k);
 bool pick_fast_literal(int N, int nfmax, FastKernels &k);
 // two-QPs-per-wave kernels (fast_pair.hip), added to k for nf <= 30 configurations
 bool add_fast_pair(int model, int N, bool fric, int nfmax, FastKernels &k);
+// workgroup-per-QP kernels (fast_wg.hip) for the instances beyond the one-wave capacity
+bool add_fast_wg(int model, int N, bool fric, FastKernels &k);
 
 #ifdef MPCQP_FAST_TU
 namespace {

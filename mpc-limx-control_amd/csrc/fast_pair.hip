@@ -31,7 +31,10 @@ void add_pair(FastKernels &k) {
 }  // namespace
 
 bool add_fast_pair(int model, int N, bool fric, int nfmax, FastKernels &k) {
-    if (fric || N != 10 || nfmax > kPairNF) return false;
+    static_assert(kPairNF == kPairCap, "one capacity");
+    // instances with more than kPairNF free forces go to the overflow list (or BAD_DIMS)
+    (void)nfmax;
+    if (fric || N != 10) return false;
     if (model == MPCQP_MODEL_SRBM && k.nu == 6) { add_pair<6, 10, 0>(k); return true; }
     if (model == MPCQP_MODEL_LITERAL && k.nu == 3) { add_pair<3, 10, 1>(k); return true; }
     return false;

@@ -1,0 +1,37 @@
+// fast_wg.hip -- the workgroup-per-QP fused kernels (mpc_wg.hpp): every contact schedule of the
+// SRBM 13/6/{10,20} configurations (double support, standing: up to 6N free forces), run on
+// the instances the one-wave kernels append to the context's overflow list.
+#include <hip/hip_runtime.h>
+
+#include "../../include/mpcqp.h"
+#include "fast_kernels.hpp"
+#include "mpc_wg.hpp"
+
+namespace mpcqp {
+namespace {
+
+// one 4-wave workgroup per QP; list != nullptr: the overflow list, else the whole batch
+template <int NU, int N, int MODEL, bool FRIC, bool GEN, int NF>
+__global__ void __launch_bounds__(kWgThreads, (NF <= 64 ? 3 : 1)) k_mpc_wg(MpcArgs a, int *list) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_w[];
+    wg_mpc_grid<NU, N, MODEL, FRIC, GEN, NF>(a, list, smem_w);
+}
+
+// explicit-input kernels only: calculateGait (the generated-input path) puts one foot down
+// per step, so a generated schedule never exceeds the one-wave capacity
+template <int N, bool FRIC, int NF>
+void add_wg(FastKernels &k) {
+    k.wg = (const void *)&k_mpc_wg<6, N, 0, FRIC, false, NF>;
+    k.wg_lds = WgSrbmLayout<6, N, FRIC, NF>::lds_bytes;
+}
+
+}  // namespace
+
+bool add_fast_wg(int model, int N, bool fric, FastKernels &k) {
+    if (model != MPCQP_MODEL_SRBM || k.nu != 6) return false;
+    if (N == 10) { fric ? add_wg<10, true, 64>(k) : add_wg<10, false, 64>(k); return true; }
+    if (N == 20) { fric ? add_wg<20, true, 128>(k) : add_wg<20, false, 128>(k); return true; }
+    return false;
+}
+
+}  // namespace mpcqp

@@ -123,6 +123,7 @@ __device__ __forceinline__ void fast_condense_solve(const FastArgs &a, unsigned 
     P.max_iter = a.max_iter;
     MPCQP_STAMP_INIT(tst);
     GiCtx C;
+    C.wide = 0;
     C.stamps = a.stamps;
     C.cut = 0;
     C.P = &P;

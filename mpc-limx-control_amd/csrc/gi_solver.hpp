@@ -112,6 +112,7 @@ struct GiCtx {
     int act, q, iters;
     unsigned long long *stamps;  // diagnostic phase cycles (nullptr: off)
     int cut;                     // diagnostic cuts build only
+    int wide;                    // 1: a workgroup solver (gi_wg.hpp) holds up to nfmax > 64
 };
 
 __device__ __forceinline__ double rowA(const SolveProblem &P, int r, int v) {
@@ -262,7 +263,7 @@ __device__ __forceinline__ void gi_setup(GiCtx &C) {
     }
     wave_sync();
     C.nf = nf;
-    if (nf > nfmax || nf > kWave) C.status = ST_BAD_DIMS;
+    if (nf > nfmax || (!C.wide && nf > kWave)) C.status = ST_BAD_DIMS;
     const int nfric = C.nfric;
     const int mt = 2 * nf + nfric + 2 * mA;
     C.mt = mt;
@@ -621,6 +622,7 @@ __device__ __forceinline__ void gi_write(GiCtx &C, const SolveOut &O) {
 __device__ __forceinline__ void wave_gi_solve(const SolveProblem &P, const SolveOut &O,
                                      unsigned char *smem, int nfmax) {
     GiCtx C;
+    C.wide = 0;
     C.stamps = nullptr;
     C.cut = 0;
     C.P = &P;

@@ -1,0 +1,533 @@
+// gi_wg.hpp -- Goldfarb-Idnani solve of ONE QP by a 4-wave workgroup, for up to NF <= 128
+// free variables: the instances the one-wave kernels cannot hold (double support / standing
+// at N = 10 and 20, up to 6N = 120 free forces) and the whole-body configuration E
+// (nV = 96).  Replaces qpOASES in QPSolver::solveQP (src/QPSolver.cpp:83-106), which the
+// reference calls on the dense nV = NU*N problem whatever the bound pattern (:87-96).
+//
+// Same algorithm, constraint order and tolerances as gi_run_reg (gi_reg.hpp), gi_run
+// (gi_solver.hpp) and the CPU oracle; only the distribution over threads differs:
+//   * 256 threads = rows 0..127 x two column halves.  Thread (r, h) (h = tid / 128, waves 0-1
+//     are half 0, waves 2-3 half 1) holds columns [h NF/2, (h+1) NF/2) of row r: first of H_FF
+//     (then L, right-looking Cholesky), then of J = L^-T Q.  NF/2 <= 64 doubles per thread.
+//   * Cholesky: step k publishes column k (and g_k) to LDS, one barrier, every thread updates
+//     its half-row.  The half that owns column k keeps its live columns at the front of its
+//     register array (each update writes column j+1's result into slot j), so the column
+//     published at step k is always slot 0: runtime loops, compile-time register indices.
+//     L is parked in LDS (column-major packed) and g rides along (t = L^-1 g).
+//   * J = L^-T by back substitution of L' J = I, one row per step: the owner of row l scales
+//     and publishes it, every row r < l subtracts L(l, r) times it.  The two halves are
+//     independent here (each column of J is its own system).
+//   * Dual loop: the most violated constraint is found by the rows of half 0 (bounds of their
+//     own variable and, for a foot's vertical force, that foot-step's friction rows); the
+//     constraint's normal n is published as J rows (d = J' n); z = J2 d2 is a per-half dot
+//     product summed over the two halves through LDS; r = R^-1 d1 and the slot bookkeeping
+//     (u, active ids, R packed in LDS) run on wave 0 (two slots per lane); the add step is
+//     the Householder reflection of gi_reg.hpp, the drop step Givens rotations whose chain
+//     crosses the half boundary once.
+//   * Sums across threads are combined in a fixed order (half 0 + half 1, wave 0 + wave 1),
+//     so both halves hold bit-identical copies of x, z and every scalar.
+#pragma once
+#include "gi_reg.hpp"
+
+namespace mpcqp {
+
+constexpr int kWgRows = 128;             // rows per column half (two waves)
+constexpr int kWgThreads = 2 * kWgRows;  // four waves
+
+// column k of the parked L, rows k..NF-1 (column-major packed, no padding)
+template <int NF>
+__device__ __forceinline__ int wg_lcol(int k) { return k * NF - (k * (k - 1)) / 2; }
+
+template <int NF>
+struct WgLayout {
+    static_assert(NF % 2 == 0 && NF >= 2 && NF <= kWgRows, "two column halves of <= 64");
+    static constexpr int NH = NF / 2;
+    static constexpr int NRP = NF * (NF + 3) / 2;    // packed L, then packed R (roff)
+    static constexpr int CBW = kWgRows + 2;          // column broadcast: 128 rows + g slot
+    static constexpr int oL = 0;
+    static constexpr int oCol = (NRP + 1) & ~1;      // [2][CBW]; then the rotations (2 NF)
+    static constexpr int oD = oCol + 2 * CBW;        // d = J' n (published rows)
+    static constexpr int oDq = oD + kWgRows;         // d masked to c >= q, then the reflector v
+    static constexpr int oD2 = oDq + kWgRows;        // second friction row; drop carry
+    static constexpr int oPart = oD2 + kWgRows;      // [2][128] per-half partial sums
+    static constexpr int oT = oPart + 2 * kWgRows;   // t = L^-1 g; drop carry
+    static constexpr int oRinv = oT + kWgRows;       // 1/L(k,k), then 1/R(j,j)
+    static constexpr int oUs = oRinv + kWgRows;      // slot multipliers u
+    static constexpr int oRed = oUs + kWgRows;       // reduction slots
+    static constexpr int oAct = oRed + 32;           // slot constraint ids (int)
+    static constexpr int doubles = oAct + kWgRows / 2;
+    static_assert(2 * CBW >= 2 * NF, "rotations fit the column buffers");
+};
+
+struct WgIds {
+    int tid, h, r, wv, ln;
+};
+__device__ __forceinline__ WgIds wg_ids() {
+    WgIds t;
+    t.tid = (int)threadIdx.x;
+    // opaque per call: the index arithmetic (and every LDS address derived from it) is
+    // recomputed per instance instead of being hoisted out of a persistent kernel's instance
+    // loop and held in registers across the whole solve
+    asm volatile("" : "+v"(t.tid));
+    // the half and the wave index are wave-uniform: in SGPRs, so the per-column LDS addresses
+    // and masks of the unrolled loops are scalar (not a VGPR per column held across the loop)
+    t.h = __builtin_amdgcn_readfirstlane(t.tid >> 7);
+    t.r = t.tid & (kWgRows - 1);
+    t.wv = __builtin_amdgcn_readfirstlane(t.tid >> 6);
+    t.ln = lane();
+    return t;
+}
+
+// lexicographic (value, id) minimum of the two half-0 wave results in red[o..o+3]
+__device__ __forceinline__ void wg_pick2(const double *red, int o, double &v, int &id) {
+    const double v0 = red[o], v1 = red[o + 2];
+    const int i0 = (int)red[o + 1], i1 = (int)red[o + 3];
+    const bool take1 = v1 < v0 || (v1 == v0 && i1 < i0);
+    v = take1 ? v1 : v0;
+    id = take1 ? i1 : i0;
+}
+
+// hr: thread (r, h) holds H_FF(r, h NF/2 + j) for c <= r (rows / columns >= nf padded with the
+// identity, so every step runs unpredicated; entries above the diagonal are never read).
+// g: g_r on both halves of row r (0 beyond nf).  W: WgLayout<NF>::doubles of LDS.
+// C.L must provide xs (128), cb, st, fid, pos, xfull.  Fills C.{status, x, fval, q, iters};
+// every thread returns x_r of its row.
+template <int NF>
+__device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double g, double *W) {
+    using Lay = WgLayout<NF>;
+    constexpr int NH = Lay::NH, CBW = Lay::CBW;
+    GiLds &L = C.L;
+    const SolveProblem &P = *C.P;
+    const WgIds T = wg_ids();
+    const int h = T.h, r = T.r, wv = T.wv, ln = T.ln, tid = T.tid;
+    const int nf = C.nf, mt = C.mt;
+    int status = C.status;
+    double *Lc = W + Lay::oL, *colb = W + Lay::oCol, *dB = W + Lay::oD, *dqB = W + Lay::oDq,
+           *d2B = W + Lay::oD2, *part = W + Lay::oPart, *tB = W + Lay::oT,
+           *rinv = W + Lay::oRinv, *us = W + Lay::oUs, *red = W + Lay::oRed;
+    double *rot = colb;
+    int *acts = reinterpret_cast<int *>(W + Lay::oAct);
+    const bool live = r < NF;
+    double x = 0.0, fval = 0.0;
+    int iters = 0, q = 0;
+    double Jr[NH];
+
+    // ---- Cholesky H_FF = L L' (right-looking) with the forward solve L t = g in the same sweep
+    double gv = (live && r < nf) ? g : 0.0;
+    if (status == ST_OK && nf > 0) {
+        bool bad = false;
+        for (int k = 0; k < nf; ++k) {
+            const int kh = k >= NH ? 1 : 0;
+            double *cb = colb + (k & 1) * CBW;
+            if (h == kh && live && r >= k) cb[r] = hr[0];  // column k (pivot at r == k)
+            if (tid == k) cb[kWgRows] = gv;                 // g_k (thread (k, 0))
+            __syncthreads();
+            const double piv = cb[k];
+            bad |= !(piv > 0.0);
+            const double isq = rsqrt_nr(piv);                // 1 / L(k,k)
+            const double hk = (live && r > k) ? cb[r] : 0.0; // H(r, k)
+            const double lr = hk * isq;                      // L(r, k)
+            const double tk = cb[kWgRows] * isq;             // t_k
+            gv = (r == k) ? tk : ((r > k) ? gv - lr * tk : gv);
+            if (h == kh && live && r >= k) Lc[wg_lcol<NF>(k) + r - k] = (r == k) ? piv * isq : lr;
+            if (tid == 0) rinv[k] = isq;
+            const double fr = hk * (isq * isq);              // L(r,k) / L(k,k)
+            if (h == kh) {
+                // this half owns column k: column k+1+j moves into slot j
+                const double *src = cb + k + 1;
+#pragma unroll
+                for (int j = 0; j < NH - 1; ++j) {
+                    hr[j] = hr[j + 1] - fr * src[j];
+                    if ((j & 7) == 7) step_fence();  // bound the loads in flight
+                }
+                hr[NH - 1] = 0.0;
+            } else if (h > kh) {
+                const double *src = cb + NH;
+#pragma unroll
+                for (int j = 0; j < NH; ++j) {
+                    hr[j] -= fr * src[j];
+                    if ((j & 7) == 7) step_fence();
+                }
+            }
+        }
+        if (bad) status = ST_NOT_PD;
+    }
+    MPCQP_CUT(C.cut, 4);
+
+    if (status == ST_OK && nf > 0) {
+        // ---- J = L^-T: back substitution of L' J = I, row l published per step
+        if (h == 0) tB[r] = (r < nf) ? gv : 0.0;
+#pragma unroll
+        for (int j = 0; j < NH; ++j) Jr[j] = (r == h * NH + j) ? 1.0 : 0.0;
+        const int lrow = live ? wg_lcol<NF>(r) - r : 0;  // L(l, r) at Lc[lrow + l], l > r
+        for (int l = nf - 1; l >= 0; --l) {
+            double *rb = colb + (l & 1) * CBW + h * NH;
+            if (r == l) {
+                const double il = rinv[l];
+#pragma unroll
+                for (int j = 0; j < NH; ++j) {
+                    Jr[j] *= il;
+                    rb[j] = Jr[j];
+                }
+            }
+            __syncthreads();
+            if (r < l) {
+                const double llr = Lc[lrow + l];
+#pragma unroll
+                for (int j = 0; j < NH; ++j) {
+                    Jr[j] -= llr * rb[j];
+                    if ((j & 7) == 7) step_fence();
+                }
+            }
+        }
+        MPCQP_CUT(C.cut, 5);
+        // ---- unconstrained minimum x = -J t, objective -|t|^2 / 2
+        double s4[4] = {0.0, 0.0, 0.0, 0.0};
+        const double *tb = tB + h * NH;
+#pragma unroll
+        for (int j = 0; j < NH; ++j) {
+            s4[j & 3] += Jr[j] * tb[j];
+            if ((j & 7) == 7) step_fence();
+        }
+        part[h * kWgRows + r] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+        if (h == 0) {
+            const double tt = wave_sum((r < nf) ? gv * gv : 0.0);
+            if (ln == 0) red[wv] = tt;
+        }
+        __syncthreads();
+        x = (r < nf) ? -(part[r] + part[kWgRows + r]) : 0.0;
+        fval = -0.5 * (red[0] + red[1]);
+        if (h == 0) L.xs[r] = x;
+        __syncthreads();
+    }
+    MPCQP_CUT(C.cut, 6);
+
+    // ---- dual active-set loop: one pass = one add or drop step
+    const int max_iter = P.max_iter > 0 ? P.max_iter : 10 * (mt + nf + 1);
+    bool done = (status != ST_OK) || nf == 0;
+    bool fresh = true;
+    int p = 0;
+    int fbase = -1;  // friction rows of the foot-step whose vertical force is variable r
+    if (C.nfric > 0 && status == ST_OK && h == 0 && r < nf) {
+        const int v = L.fid[r], k = v / P.nu, c = v % P.nu, sft = c / 3;
+        if (c % 3 == 2 && ((P.contact >> (2 * k + sft)) & 1ull)) fbase = 2 * nf + 4 * (k * P.nfeet + sft);
+    }
+    while (!done) {
+        if (fresh) {
+            // ---- step 1: most violated inactive constraint (lowest id on ties)
+            double best = INFINITY;
+            int bid = 0x7fffffff;
+            if (h == 0 && r < nf) {
+                const unsigned char s0 = L.st[r], s1 = L.st[r + nf];
+                const double b0 = L.cb[r], b1 = L.cb[r + nf];
+                if (s0 == 1) {
+                    const double sl_ = x - b0;
+                    if (sl_ < -kFeasTol * (1.0 + fabs(b0))) { best = sl_; bid = r; }
+                }
+                if (s1 == 1) {
+                    const double sl_ = -x - b1;
+                    if (sl_ < -kFeasTol * (1.0 + fabs(b1)) && sl_ < best) { best = sl_; bid = r + nf; }
+                }
+                if (fbase >= 0) {
+                    const double xm1 = L.xs[r - 1], xm2 = L.xs[r - 2];  // fy, fx of the foot
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        if (L.st[fbase + t] != 1) continue;
+                        const double sg = (t & 1) ? 1.0 : -1.0;
+                        double s = 0.0;
+                        s += P.mu * x;
+                        s += sg * ((t >> 1) ? xm1 : xm2);
+                        if (s < -kFeasTol && s < best) { best = s; bid = fbase + t; }
+                    }
+                }
+            }
+            wave_argmin(best, bid);
+            if (h == 0 && ln == 0) { red[4 + 2 * wv] = best; red[5 + 2 * wv] = (double)bid; }
+            __syncthreads();
+            wg_pick2(red, 4, best, bid);
+            if (bid == 0x7fffffff) break;  // optimal
+            p = bid;
+            if (tid == 0) us[q] = 0.0;
+            fresh = false;
+        }
+        // ---- d = J' n_p (published J rows) and the slack of p
+        int a0, a1 = -1;
+        double c0, c1 = 0.0, bp;
+        if (p < 2 * nf) {
+            a0 = p < nf ? p : p - nf;
+            c0 = p < nf ? 1.0 : -1.0;
+            bp = L.cb[p];
+        } else {
+            const int rr = p - 2 * nf, ks = rr >> 2, t = rr & 3;
+            const int k = ks / P.nfeet, sft = ks % P.nfeet;
+            const int pz = L.pos[k * P.nu + 3 * sft + 2], pt = L.pos[k * P.nu + 3 * sft + (t >> 1)];
+            const double sg = (t & 1) ? 1.0 : -1.0;
+            a0 = pz >= 0 ? pz : pt;
+            c0 = pz >= 0 ? P.mu : sg;
+            if (pz >= 0 && pt >= 0) { a1 = pt; c1 = sg; }
+            bp = gi_cons_b(C, p);
+        }
+        const double sp = c0 * L.xs[a0] + (a1 >= 0 ? c1 * L.xs[a1] : 0.0) - bp;
+        if (a1 < 0) {
+            if (r == a0) {
+#pragma unroll
+                for (int j = 0; j < NH; ++j) {
+                    const int c = h * NH + j;
+                    const double v = c0 * Jr[j];
+                    dB[c] = v;
+                    dqB[c] = (c >= q) ? v : 0.0;
+                    if ((j & 7) == 7) step_fence();
+                }
+            }
+        } else {
+            if (r == a0) {
+#pragma unroll
+                for (int j = 0; j < NH; ++j) {
+                    dB[h * NH + j] = c0 * Jr[j];
+                    if ((j & 7) == 7) step_fence();
+                }
+            }
+            if (r == a1) {
+#pragma unroll
+                for (int j = 0; j < NH; ++j) {
+                    d2B[h * NH + j] = c1 * Jr[j];
+                    if ((j & 7) == 7) step_fence();
+                }
+            }
+            __syncthreads();
+            if (tid < NF) {
+                const double v = dB[tid] + d2B[tid];
+                dB[tid] = v;
+                dqB[tid] = (tid >= q) ? v : 0.0;
+            }
+        }
+        __syncthreads();
+        const double uq = us[q];
+        // ---- step 2
+        if (iters >= max_iter) { status = ST_ITER_LIMIT; break; }
+        ++iters;
+        {   // z = J2 d2 (per-half partial sums)
+            double z4[4] = {0.0, 0.0, 0.0, 0.0};
+            const double *dq = dqB + h * NH;
+#pragma unroll
+            for (int j = 0; j < NH; ++j) {
+                z4[j & 3] += Jr[j] * dq[j];
+                if ((j & 7) == 7) step_fence();
+            }
+            part[h * kWgRows + r] = (z4[0] + z4[1]) + (z4[2] + z4[3]);
+        }
+        if (h == 0) {  // |d|^2, |d2|^2, |d2|^2 without d_q: thread r owns d_r
+            const double dv = (r < nf) ? dB[r] : 0.0;
+            double dd = dv * dv, zn = (r >= q) ? dv * dv : 0.0, zq = (r > q) ? dv * dv : 0.0;
+            wave_sum3(dd, zn, zq);
+            if (ln == 0) { red[8 + 3 * wv] = dd; red[9 + 3 * wv] = zn; red[10 + 3 * wv] = zq; }
+        }
+        double r0 = 0.0, r1 = 0.0;  // wave 0: r of slots ln and ln + 64
+        if (wv == 0 && q > 0) {
+            // r = R^-1 d(0:q), back substitution (R packed in LDS, 1/R(j,j) beside it)
+            double v0 = (ln < q) ? dB[ln] : 0.0, v1 = (ln + 64 < q) ? dB[ln + 64] : 0.0;
+            int j = q - 1;
+            double ra = (ln < j) ? Lc[roff(j) + ln] : 0.0;
+            double rb = (ln + 64 < j) ? Lc[roff(j) + ln + 64] : 0.0;
+            for (; j >= 0; --j) {
+                // prefetch column j - 1 while column j is applied
+                const double na = (j > 0 && ln < j - 1) ? Lc[roff(j - 1) + ln] : 0.0;
+                const double nb = (j > 0 && ln + 64 < j - 1) ? Lc[roff(j - 1) + ln + 64] : 0.0;
+                const double rj = (j < 64 ? readlane(v0, j) : readlane(v1, j - 64)) * rinv[j];
+                if (ln == j) r0 = rj;
+                if (ln + 64 == j) r1 = rj;
+                if (ln < j) v0 -= ra * rj;
+                if (ln + 64 < j) v1 -= rb * rj;
+                ra = na;
+                rb = nb;
+            }
+            const double rmax = wave_max(fmax(ln < q ? fabs(r0) : 0.0, ln + 64 < q ? fabs(r1) : 0.0));
+            double t1 = INFINITY;
+            int ks = 0x7fffffff;
+            if (ln < q && r0 > kRTol * rmax) { t1 = us[ln] / r0; ks = ln; }
+            if (ln + 64 < q && r1 > kRTol * rmax) {
+                const double tt = us[ln + 64] / r1;
+                if (tt < t1) { t1 = tt; ks = ln + 64; }
+            }
+            wave_argmin(t1, ks);
+            if (ln == 0) { red[16] = t1; red[17] = (double)ks; }
+        }
+        __syncthreads();
+        const double z = part[r] + part[kWgRows + r];
+        const double dd = red[8] + red[11], zn = red[9] + red[12], zq = red[10] + red[13];
+        double t1 = INFINITY;
+        int kslot = 0x7fffffff;
+        if (q > 0) { t1 = red[16]; kslot = (int)red[17]; }
+        const bool dep = !(zn > kDepTol * dd);
+        const double t2 = dep ? INFINITY : -sp / zn;
+        const double t = t1 < t2 ? t1 : t2;
+        if (isinf(t)) { status = ST_INFEASIBLE; break; }
+        if (!isinf(t2)) {
+            if (r < nf) x += t * z;
+            if (h == 0) L.xs[r] = x;
+            fval += t * zn * (0.5 * t + uq);
+        }
+        if (wv == 0) {
+            double u0 = us[ln], u1 = us[ln + 64];
+            if (ln < q) u0 -= t * r0;
+            if (ln == q) u0 += t;
+            if (ln + 64 < q) u1 -= t * r1;
+            if (ln + 64 == q) u1 += t;
+            us[ln] = u0;
+            us[ln + 64] = u1;
+        }
+        const bool add = !isinf(t2) && t2 <= t1;
+        if (add) {
+            // ---- add p: the Householder reflection of gi_reg.hpp, v = d2 - |d2| e_q
+            const double dq = dB[q];
+            double rqq = dq, vq = 0.0, beta = 0.0;
+            if (zq > 0.0) {
+                const double nrm = sqrt(zn);
+                rqq = nrm;
+                vq = dq > 0.0 ? -zq / (dq + nrm) : dq - nrm;
+                beta = 2.0 / (vq * vq + zq);
+            }
+            if (wv == 0) {
+                if (ln < q) Lc[roff(q) + ln] = dB[ln];
+                if (ln + 64 < q) Lc[roff(q) + ln + 64] = dB[ln + 64];
+                if (ln == 0) {
+                    Lc[roff(q) + q] = rqq;
+                    rinv[q] = 1.0 / rqq;
+                    acts[q] = p;
+                    L.st[p] = 2;
+                    dqB[q] = vq;
+                }
+            }
+            ++q;
+            fresh = true;
+            __syncthreads();
+            if (beta != 0.0) {
+                double w4[4] = {0.0, 0.0, 0.0, 0.0};
+                const double *v = dqB + h * NH;
+#pragma unroll
+                for (int j = 0; j < NH; ++j) {
+                    w4[j & 3] += Jr[j] * v[j];
+                    if ((j & 7) == 7) step_fence();
+                }
+                part[h * kWgRows + r] = (w4[0] + w4[1]) + (w4[2] + w4[3]);
+                __syncthreads();
+                const double f = beta * (part[r] + part[kWgRows + r]);
+#pragma unroll
+                for (int j = 0; j < NH; ++j) {
+                    Jr[j] -= f * v[j];
+                    if ((j & 7) == 7) step_fence();
+                }
+            }
+        } else {
+            // ---- drop slot kslot (wave 0): shift the slots and R's columns left, then Givens
+            //      back to triangular; the rotations go to LDS for J
+            const int k = kslot;
+            if (wv == 0) {
+                const int dropped = acts[k];
+                const double un0 = us[ln + 1], un1 = (ln + 65 < kWgRows) ? us[ln + 65] : 0.0;
+                const int an0 = acts[ln + 1], an1 = (ln + 65 < kWgRows) ? acts[ln + 65] : 0;
+                wave_sync();
+                if (ln >= k && ln < q - 1) { us[ln] = un0; acts[ln] = an0; }
+                if (ln + 64 >= k && ln + 64 < q - 1) { us[ln + 64] = un1; acts[ln + 64] = an1; }
+                if (ln == 0) L.st[dropped] = 1;
+                for (int j = k; j < q - 1; ++j) {
+                    const double v0 = (ln <= j + 1) ? Lc[roff(j + 1) + ln] : 0.0;
+                    const double v1 = (ln + 64 <= j + 1) ? Lc[roff(j + 1) + ln + 64] : 0.0;
+                    if (ln <= j + 1) Lc[roff(j) + ln] = v0;
+                    if (ln + 64 <= j + 1) Lc[roff(j) + ln + 64] = v1;
+                }
+                const int qn = q - 1;
+                for (int j = ln; j < NF; j += kWave) { rot[2 * j] = 1.0; rot[2 * j + 1] = 0.0; }
+                wave_sync();
+                for (int j = k; j < qn; ++j) {
+                    const double a_ = Lc[roff(j) + j], bb = Lc[roff(j) + j + 1];
+                    if (bb != 0.0) {
+                        const double hh = sqrt(a_ * a_ + bb * bb);
+                        const double ih = 1.0 / hh;
+                        const double c = a_ * ih, s_ = bb * ih;
+#pragma unroll
+                        for (int o = 0; o < 2; ++o) {
+                            const int l = j + 1 + ln + 64 * o;
+                            if (l < qn) {
+                                const double y0 = Lc[roff(l) + j], y1 = Lc[roff(l) + j + 1];
+                                Lc[roff(l) + j] = c * y0 + s_ * y1;
+                                Lc[roff(l) + j + 1] = -s_ * y0 + c * y1;
+                            }
+                        }
+                        if (ln == 0) {
+                            Lc[roff(j) + j] = hh;
+                            Lc[roff(j) + j + 1] = 0.0;
+                            rinv[j] = ih;
+                            rot[2 * j] = c;
+                            rot[2 * j + 1] = s_;
+                        }
+                    } else if (ln == 0) {
+                        rinv[j] = 1.0 / a_;  // the shifted column's diagonal as it is
+                    }
+                    wave_sync();
+                }
+            }
+            --q;
+            // J columns: rotations (j, j+1), j = 0 .. NF-2, identity where (c, s) = (1, 0);
+            // half 0 applies 0 .. NH-1 (the last one needs column NH from half 1), then half 1
+            // continues from the carried column NH
+            if (h == 1) d2B[r] = Jr[0];
+            __syncthreads();
+            if (h == 0) {
+#pragma unroll
+                for (int j = 0; j < NH - 1; ++j) {
+                    const double c = rot[2 * j], s_ = rot[2 * j + 1];
+                    const double y0 = Jr[j], y1 = Jr[j + 1];
+                    Jr[j] = c * y0 + s_ * y1;
+                    Jr[j + 1] = -s_ * y0 + c * y1;
+                }
+                const double c = rot[2 * (NH - 1)], s_ = rot[2 * (NH - 1) + 1];
+                const double y0 = Jr[NH - 1], y1 = d2B[r];
+                Jr[NH - 1] = c * y0 + s_ * y1;
+                tB[r] = -s_ * y0 + c * y1;
+            }
+            __syncthreads();
+            if (h == 1) {
+                Jr[0] = tB[r];
+#pragma unroll
+                for (int j = 0; j < NH - 1; ++j) {
+                    const double c = rot[2 * (NH + j)], s_ = rot[2 * (NH + j) + 1];
+                    const double y0 = Jr[j], y1 = Jr[j + 1];
+                    Jr[j] = c * y0 + s_ * y1;
+                    Jr[j + 1] = -s_ * y0 + c * y1;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    MPCQP_CUT(C.cut, 7);
+    C.status = status;
+    C.x = x;
+    C.fval = fval;
+    C.q = q;
+    C.iters = iters;
+    C.u = 0.0;
+    C.act = -1;
+}
+
+// outputs of a workgroup solve: x of the free variables from the rows of half 0, fixed values,
+// cost / status / iterations (gi_write's conventions)
+__device__ __forceinline__ void gi_write_wg(GiCtx &C, const SolveOut &O) {
+    const SolveProblem &P = *C.P;
+    GiLds &L = C.L;
+    const WgIds T = wg_ids();
+    const int nV = P.nV, nf = C.nf;
+    const bool have_map = nf <= C.nfmax;
+    for (int v = T.tid; v < nV; v += kWgThreads) {
+        const int pv = L.pos[v];
+        if (pv < 0 || !have_map) O.x[v] = (pv < 0) ? L.xfull[v] : 0.0;
+    }
+    if (have_map && T.h == 0 && T.r < nf) O.x[L.fid[T.r]] = C.x;
+    if (T.tid == 0) {
+        *O.cost = C.fval + C.c0;
+        *O.status = C.status;
+        *O.iters = C.iters;
+    }
+}
+
+}  // namespace mpcqp

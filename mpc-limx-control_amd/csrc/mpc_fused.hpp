@@ -49,7 +49,15 @@ struct MpcArgs {
     const double *phase;  // [S * cands] gait phase of each candidate at step 0 (s)
     int cands;
     float swing, stance;  // MPCParam::swing_time / stance_time (float, include/MPCParam.h:48-49)
+    int *ovf;  // overflow list (mpc_wg.hpp) for instances beyond the kernel's free capacity
 };
+
+// overflow list layout (int): [0] count, [1] exit ticket, [2 ..] instance ids
+constexpr int kListHead = 2;
+__device__ __forceinline__ void wg_list_append(int *list, int b) {
+    const int i = __hip_atomic_fetch_add(&list[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    list[kListHead + i] = b;
+}
 
 // Gait contact mask of one horizon: MPC::calculateGait (include/MPCController.h:61-75)
 // evaluated at phase0 + k Ts for k = 0..N-1 (lane k, exact fmod as the host's math.fmod);
@@ -145,56 +153,20 @@ __device__ __forceinline__ void beta_sums(int m0, int m1, int ki, int kj, double
     sij = s2 - (oi + oj) * s1 + oi * oj * n;
 }
 
-template <int NU, int N, int MODEL, bool FRIC, int NF, bool GEN = false>
-__device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) {
-    static_assert(!GEN || MODEL == 0, "generated inputs are defined for the SRBM model");
-    using Lay = MpcLayout<NU, N, FRIC, NF>;
-    constexpr int NX = 13, NS = NX + NU, NV = Lay::NV, LD = Lay::LD;
-    const int b = blockIdx.x, ln = lane();
-    double *D = reinterpret_cast<double *>(smem);
-    double *X0 = D + Lay::oX0, *X1 = D + Lay::oX1, *S = D + Lay::oS, *UV = D + Lay::oUV;
-    static_assert(MODEL == 0 || MODEL == 1, "TRON1 models only");
-    double *Ax = D + Lay::oAx, *A2x = Ax + NX;
-    MPCQP_STAMP_INIT(tst);
+// ---- phases of the fused step shared by the one-wave kernel (fast_mpc below) and the
+//      workgroup kernel (mpc_wg.hpp); each runs on ONE wave.  Lay provides the LDS offsets
+//      (doubles from D): oXr, oX0v, oRm, oT, oX0, oX1, oAx, oS, oUV.
 
-    // ---- solver context (bounds from the contact schedule)
-    SolveProblem P;
-    P.nV = NV;
-    P.H = nullptr; P.f = nullptr; P.lb = nullptr; P.ub = nullptr;
-    P.gen_bounds = 1;
-    P.model = MODEL; P.nu = NU; P.N = N; P.nfeet = 2;
-    P.fz_min = a.fz_min; P.fz_max = a.fz_max; P.fxy_max = a.fxy_max;
-    P.u_min = a.u_min; P.u_max = a.u_max;
+// per-instance inputs of instance b (x0, xref, R, lin)
+template <class Lay, int NU, int N, bool GEN>
+__device__ __forceinline__ void mpc_load_inputs(const MpcArgs &a, int b, double *D,
+                                                double (&lin)[8]) {
+    constexpr int NX = 13;
+    const int ln = lane();
     const int st_ = GEN ? b / a.cands : b;  // state row of this instance (GEN)
-    P.contact = (MODEL != 0) ? 0ull
-              : GEN ? gait_mask_wave(N, a.Ts, a.phase[b], a.swing, a.stance) : a.contact[b];
-    P.friction = FRIC ? 1 : 0;
-    P.mu = a.mu;
-    P.mA = 0; P.A = nullptr; P.a_colmajor = 0; P.lbA = nullptr; P.ubA = nullptr;
-    P.max_iter = a.max_iter;
-    GiCtx C;
-    C.stamps = a.stamps;
-    C.cut = a.cut;
-    C.P = &P;
-    C.nfmax = NF;
-    C.L.ld = LD;
-    C.L.R = D + Lay::oR;
-    C.L.J = nullptr;
-    C.L.g = nullptr;
-    C.L.xs = D + Lay::oXS;
-    C.L.xfull = D + Lay::oXF;
-    C.L.rowfix = D + Lay::oMisc;
-    C.L.ys = D + Lay::oMisc;
-    int *ip = reinterpret_cast<int *>(D + Lay::nDoubles);
-    C.L.fid = ip;
-    C.L.pos = ip + NF;
-    C.L.st = reinterpret_cast<unsigned char *>(ip + NF + NV);
-    C.L.cb = D + Lay::oCB;
-
     // ---- per-instance inputs: all global loads issued back to back (one HBM round trip),
     //      then parked in LDS
     double *xr = D + Lay::oXr, *x0g = D + Lay::oX0v;
-    double lin[8];
     if constexpr (GEN) {
         // x0 = the state; xref as mpcQP::mpcQP builds it (include/mpcQP.h:74-97) from the
         // state and the (yaw rate, forward speed) command; lin = {yaw, r_L, r_R}
@@ -235,14 +207,21 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
         if (ln < NX) x0g[ln] = x0l;
         if (ln < NU * NU) D[Lay::oRm + ln] = rml;
     }
-    (void)st_;
-    // ---- model: X0 = Bc Ts, X1 = (Ac Ts)(Bc Ts); A x0, A^2 x0
     wave_sync();
-    MPCQP_CUT(a.cut, 11);
+    (void)st_;
+}
+
+// model: X0 = Bc Ts, X1 = (Ac Ts)(Bc Ts); A x0, A^2 x0
+template <class Lay, int NU, int MODEL>
+__device__ __forceinline__ void mpc_model_terms(const MpcArgs &a, double *D,
+                                                const double (&lin)[8]) {
+    constexpr int NX = 13, NS = NX + NU;
+    const int ln = lane();
+    double *X0 = D + Lay::oX0, *X1 = D + Lay::oX1, *Ax = D + Lay::oAx, *A2x = Ax + NX;
+    double *x0g = D + Lay::oX0v;
     double Iwi[9];
     double cy = 1.0, sy = 0.0;
     if (MODEL == 0) srbm_rot_inertia(lin[0], a.Ibinv, cy, sy, Iwi);
-    MPCQP_CUT(a.cut, 12);
     auto entry = [&](int i, int j) -> double {  // [Ac | Bc](i, j)
         return MODEL == 0 ? srbm_entry(i, j, lin, cy, sy, Iwi, a.mass)
                           : literal_entry(i, j, lin, a.mass);
@@ -278,13 +257,16 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
         A2x[ln] = s * Ts;
     }
     wave_sync();
-    MPCQP_CUT(a.cut, 13);
-    gi_setup(C);  // free map + constraint states
-    if (C.nf > a.max_free) C.status = ST_BAD_DIMS;
-    wave_sync();
-    MPCQP_STAMP(a.stamps, 0, tst);
-    MPCQP_CUT(a.cut, 1);
+}
 
+// condensed terms: the S^W blocks and u_m / v_m
+template <class Lay, int NU, int N, int MODEL>
+__device__ __forceinline__ void mpc_condensed_terms(const MpcArgs &a, double *D) {
+    constexpr int NX = 13;
+    const int ln = lane();
+    double *X0 = D + Lay::oX0, *X1 = D + Lay::oX1, *S = D + Lay::oS, *UV = D + Lay::oUV;
+    double *Ax = D + Lay::oAx, *A2x = Ax + NX;
+    double *xr = D + Lay::oXr, *x0g = D + Lay::oX0v;
     // ---- S^W_rr = X_r' W X_r over the support rows (w: 0 = Q, 1 = P); slot blk = 2w + r of
     //      entry o = cj NU + ci (the cross blocks X0' W X1 are zero and not stored).
     //      The block loop is wave-uniform so the weights are scalar loads.
@@ -321,6 +303,97 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
         UV[(m * 2 + 1) * NU + c] = sv;
     }
     wave_sync();
+}
+
+// H_FF(vi, vj) and g(vi) of the condensed problem from the terms above (closed form; the
+// cross blocks X0' W X1 vanish, XSupport)
+template <class Lay, int NU, int N>
+__device__ __forceinline__ double mpc_h_entry(const double *D, int vi, int vj) {
+    const int ki = vi / NU, ci = vi % NU, kj = vj / NU, cj = vj % NU;
+    const int kk = ki > kj ? ki : kj;
+    double c, si, sj, sij;
+    beta_sums(kk + 1, N - 1, ki, kj, c, si, sj, sij);
+    const double bi = (double)(N - 1 - ki) + 0.5, bj = (double)(N - 1 - kj) + 0.5;
+    const double *So = D + Lay::oS + (cj * NU + ci) * 4;
+    double v = c * So[0] + sij * So[1];
+    v += So[2] + bi * bj * So[3];
+    if (ki == kj) v += D[Lay::oRm + cj * NU + ci];
+    return 2.0 * v;
+}
+template <class Lay, int NU, int N>
+__device__ __forceinline__ double mpc_g_entry(const double *D, int vi) {
+    const int ki = vi / NU, ci = vi % NU;
+    const double *UV = D + Lay::oUV;
+    double s = 0.0;
+    for (int m = ki + 1; m <= N; ++m) {
+        const double beta = (double)(m - 1 - ki) + 0.5;
+        s += UV[(m * 2 + 0) * NU + ci] + beta * UV[(m * 2 + 1) * NU + ci];
+    }
+    return 2.0 * s;
+}
+
+template <int NU, int N, int MODEL, bool FRIC, int NF, bool GEN = false>
+__device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) {
+    static_assert(!GEN || MODEL == 0, "generated inputs are defined for the SRBM model");
+    using Lay = MpcLayout<NU, N, FRIC, NF>;
+    constexpr int NX = 13, NS = NX + NU, NV = Lay::NV, LD = Lay::LD;
+    const int b = blockIdx.x, ln = lane();
+    double *D = reinterpret_cast<double *>(smem);
+    double *X0 = D + Lay::oX0, *X1 = D + Lay::oX1, *S = D + Lay::oS, *UV = D + Lay::oUV;
+    static_assert(MODEL == 0 || MODEL == 1, "TRON1 models only");
+    double *Ax = D + Lay::oAx, *A2x = Ax + NX;
+    MPCQP_STAMP_INIT(tst);
+
+    // ---- solver context (bounds from the contact schedule)
+    SolveProblem P;
+    P.nV = NV;
+    P.H = nullptr; P.f = nullptr; P.lb = nullptr; P.ub = nullptr;
+    P.gen_bounds = 1;
+    P.model = MODEL; P.nu = NU; P.N = N; P.nfeet = 2;
+    P.fz_min = a.fz_min; P.fz_max = a.fz_max; P.fxy_max = a.fxy_max;
+    P.u_min = a.u_min; P.u_max = a.u_max;
+    P.contact = (MODEL != 0) ? 0ull
+              : GEN ? gait_mask_wave(N, a.Ts, a.phase[b], a.swing, a.stance) : a.contact[b];
+    P.friction = FRIC ? 1 : 0;
+    P.mu = a.mu;
+    P.mA = 0; P.A = nullptr; P.a_colmajor = 0; P.lbA = nullptr; P.ubA = nullptr;
+    P.max_iter = a.max_iter;
+    GiCtx C;
+    C.wide = 0;
+    C.stamps = a.stamps;
+    C.cut = a.cut;
+    C.P = &P;
+    C.nfmax = NF;
+    C.L.ld = LD;
+    C.L.R = D + Lay::oR;
+    C.L.J = nullptr;
+    C.L.g = nullptr;
+    C.L.xs = D + Lay::oXS;
+    C.L.xfull = D + Lay::oXF;
+    C.L.rowfix = D + Lay::oMisc;
+    C.L.ys = D + Lay::oMisc;
+    int *ip = reinterpret_cast<int *>(D + Lay::nDoubles);
+    C.L.fid = ip;
+    C.L.pos = ip + NF;
+    C.L.st = reinterpret_cast<unsigned char *>(ip + NF + NV);
+    C.L.cb = D + Lay::oCB;
+
+    double lin[8];
+    mpc_load_inputs<Lay, NU, N, GEN>(a, b, D, lin);
+    MPCQP_CUT(a.cut, 11);
+    mpc_model_terms<Lay, NU, MODEL>(a, D, lin);
+    MPCQP_CUT(a.cut, 13);
+    gi_setup(C);  // free map + constraint states
+    if (C.nf > a.max_free) C.status = ST_BAD_DIMS;
+    wave_sync();
+    if (a.ovf && C.nf > NF && C.nf <= a.max_free) {  // the workgroup kernel takes it
+        if (ln == 0) wg_list_append(a.ovf, b);
+        return;
+    }
+    MPCQP_STAMP(a.stamps, 0, tst);
+    MPCQP_CUT(a.cut, 1);
+
+    mpc_condensed_terms<Lay, NU, N, MODEL>(a, D);
     MPCQP_STAMP(a.stamps, 1, tst);
     MPCQP_CUT(a.cut, 2);
 

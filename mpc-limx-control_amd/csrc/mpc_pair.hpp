@@ -768,7 +768,10 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     MPCQP_CUT(a.cut, 7);
     // ---- outputs
     const int bo = (int)(long long)ctl[1];
-    if (bo >= 0) {
+    const bool defer = a.ovf && nf > NF && nf <= a.max_free;  // the workgroup kernel takes it
+    if (bo >= 0 && defer) {
+        if (hl == 0) wg_list_append(a.ovf, bo);
+    } else if (bo >= 0) {
         const uint64_t cto = *ctl;
         double *U = a.U + (size_t)bo * NV;
         const bool have_map = nf <= NF;

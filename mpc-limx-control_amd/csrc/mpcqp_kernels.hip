@@ -27,6 +27,7 @@
 
 #include "fast_kernels.hpp"
 #include "gi_solver.hpp"
+#include "gi_wg.hpp"
 
 using namespace mpcqp;
 
@@ -417,15 +418,23 @@ bool pair_enabled() {
 
 // instantiated configurations (BASELINE configs A/B/C and the literal model); anything else
 // runs the generic runtime-dimension kernels
+// The one-wave kernel is sized for min(nfmax, 64) free variables; an SRBM context whose nfmax
+// exceeds what its one-wave kernel holds (30 for the paired kernel, NF for k_mpc) also gets the
+// workgroup kernel (fast_wg.hip) for the instances beyond it (the overflow list).
 bool pick_fast(int model, int nx, int nu, int N, bool fric, int nfmax, FastKernels &k) {
     if (nx != 13) return false;
     bool found = false;
+    const int nprim = std::min(nfmax, 64);
     if (model == MPCQP_MODEL_SRBM && nu == 6) {
-        if (N == 10) found = pick_fast_srbm10(fric, nfmax, k);
-        if (N == 20) found = pick_fast_srbm20(fric, nfmax, k);
+        if (N == 10) found = pick_fast_srbm10(fric, nprim, k);
+        if (N == 20) found = pick_fast_srbm20(fric, nprim, k);
     }
-    if (model == MPCQP_MODEL_LITERAL && nu == 3 && !fric) found = pick_fast_literal(N, nfmax, k);
-    if (found && pair_enabled()) add_fast_pair(model, N, fric, nfmax, k);
+    if (model == MPCQP_MODEL_LITERAL && nu == 3 && !fric) found = pick_fast_literal(N, nprim, k);
+    if (found && pair_enabled()) add_fast_pair(model, N, fric, nprim, k);
+    if (found) {
+        k.prim_nf = k.pair ? kPairCap : (nprim <= 32 ? 32 : 64);
+        if (nfmax > k.prim_nf) add_fast_wg(model, N, fric, k);
+    }
     return found;
 }
 
@@ -509,6 +518,9 @@ struct mpcqp_ctx {
     size_t ab_cap = 0;
     unsigned long long *dstamps = nullptr;  // diagnostic phase cycles (stamps build)
     unsigned long long *dsel = nullptr;     // k_select_min: per-block partial keys + ticket
+    int *dlist = nullptr;                   // overflow list [count, ticket, ids...] (mpc_wg.hpp)
+    size_t list_cap = 0;                    // instances the list holds
+    int wg_grid = 0;                        // resident workgroups of the workgroup kernel
     // host-pointer entry point staging
     void *hbuf = nullptr;
     size_t hbuf_cap = 0;
@@ -677,7 +689,7 @@ int mpcqp_solve_dense(int nV, int nC, const double *H, const double *f, const do
         const double lo = lb ? lb[i] : -MPCQP_INFTY, hi = ub ? ub[i] : MPCQP_INFTY;
         if (lo != hi) ++nfree;
     }
-    if (nfree > MPCQP_MAX_FREE) return MPCQP_ERR_BAD_DIMS;
+    if (nfree > kWave) return MPCQP_ERR_BAD_DIMS;  // the one-wave dense solver
     const int nfmax = std::max(1, nfree);
     SolveArgs a;
     memset(&a, 0, sizeof(a));
@@ -791,6 +803,17 @@ int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
                            (m->fz_min < m->fz_max && m->fxy_max > 0.0);
     c->fast = is_diag(m->Q, nx) && is_diag(m->P, nx) && bounds_ok && nu <= 6 &&
               pick_fast(m->model, nx, nu, m->N, fric, nfmax, c->fk);
+    if (!c->fast && nfmax > kWave) {  // the generic one-wave solver holds 64 free variables
+        mpcqp_ctx_destroy(c);
+        return MPCQP_ERR_BAD_DIMS;
+    }
+    if (c->fast && c->fk.wg) {  // resident grid of the persistent workgroup kernels
+        int dev_cus = 0, nb = 0;
+        hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, device);
+        set_lds(c->fk.wg, c->fk.wg_lds);
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, c->fk.wg, kWgThreads, c->fk.wg_lds);
+        c->wg_grid = std::max(1, nb) * std::max(1, dev_cus);
+    }
     c->m.Q = c->m.R = c->m.P = nullptr;  // host pointers are not kept
     c->ev_ok = true;
     for (int i = 0; i < 6; ++i)
@@ -840,6 +863,7 @@ int mpcqp_ctx_destroy(mpcqp_ctx *c) {
     hipFree(c->dAB);
     hipFree(c->dstamps);
     hipFree(c->dsel);
+    hipFree(c->dlist);
     hipFree(c->hbuf);
     hipFree(c->rbuf);
     hipFree(c->scratchH);
@@ -958,11 +982,39 @@ static int launch(const void *k, int B, size_t lds, hipStream_t s, void *arg) {
     return hip_status(hipLaunchKernel(k, dim3(B), dim3(64), args, lds, s));
 }
 
-// the fused step: two instances per wave when the paired kernel is instantiated
+// overflow list for B instances (grown on demand; mpcqp_ctx_reserve sizes it up front)
+static int ensure_list(mpcqp_ctx *c, int B) {
+    if (c->list_cap >= (size_t)B) return MPCQP_OK;
+    if (c->dlist) hipStreamSynchronize(c->stream);
+    hipFree(c->dlist);
+    c->dlist = nullptr;
+    c->list_cap = 0;
+    if (hipMalloc(&c->dlist, sizeof(int) * (kListHead + (size_t)B)) != hipSuccess ||
+        hipMemsetAsync(c->dlist, 0, sizeof(int) * kListHead, c->stream) != hipSuccess)
+        return MPCQP_ERR_DEVICE;
+    c->list_cap = B;
+    return MPCQP_OK;
+}
+
+// the fused step: two instances per wave when the paired kernel is instantiated; instances
+// beyond the one-wave kernel's free capacity go through the overflow list to the workgroup
+// kernel, launched right after on the same stream
 static int launch_mpc(mpcqp_ctx *c, bool gen, int B, MpcArgs *a) {
+    a->ovf = nullptr;
+    if (c->fk.wg && !gen) {
+        const int rc = ensure_list(c, B);
+        if (rc) return rc;
+        a->ovf = c->dlist;
+    }
     const void *pk = gen ? c->fk.pair_gen : c->fk.pair;
-    if (pk) return launch(pk, (B + 1) / 2, c->fk.pair_lds, c->stream, a);
-    return launch(gen ? c->fk.mpc_gen : c->fk.mpc, B, c->fk.mpc_lds, c->stream, a);
+    int rc = pk ? launch(pk, (B + 1) / 2, c->fk.pair_lds, c->stream, a)
+                : launch(gen ? c->fk.mpc_gen : c->fk.mpc, B, c->fk.mpc_lds, c->stream, a);
+    if (rc || !a->ovf) return rc;
+    int *list = c->dlist;
+    void *args[] = {a, &list};
+    const int grid = std::max(1, std::min(B, c->wg_grid));
+    return hip_status(hipLaunchKernel(c->fk.wg, dim3(grid), dim3(kWgThreads), args, c->fk.wg_lds,
+                                      c->stream));
 }
 
 int mpcqp_batch_condense(mpcqp_ctx *c, int B, const double *x0, const double *xref,
@@ -986,7 +1038,8 @@ static SolveArgs batch_solve_args(mpcqp_ctx *c, int B, const double *H, const do
     memset(&a, 0, sizeof(a));
     const mpcqp_model &m = c->m;
     a.B = B;
-    a.nfmax = m.max_free > 0 ? m.max_free : m.nu * m.N;
+    // the stand-alone solve is one wave: at most 64 free variables (more -> BAD_DIMS)
+    a.nfmax = std::min(kWave, m.max_free > 0 ? m.max_free : m.nu * m.N);
     a.P.nV = m.nu * m.N;
     a.P.H = H;
     a.P.f = f;

@@ -72,7 +72,7 @@ inline ModelSpec srbm_model(int N, bool friction) {
     m.u_min = -8.0;
     m.u_max = 8.0;
     m.max_iter = 0;
-    m.max_free = 3 * N;
+    m.max_free = 0;  // nu N: every contact schedule (double support, standing)
     s.rebind();
     return s;
 }

@@ -73,7 +73,7 @@ def model_params(config: str = "B", N: int | None = None) -> dict:
                 constraints=cons, Ts=TS, mass=MASS, mu=MU, Ib=INERTIA.copy(), fz_min=0.0,
                 fz_max=fzmax, fxy_max=MU * fzmax, u_min=-8.0, u_max=8.0, Q=Q,
                 R=(R_SRBM if model == MODEL_SRBM else 0.1) * np.eye(nu), P=20.0 * Q, max_iter=0,
-                max_free=(3 * Nh if model == MODEL_SRBM else nu * Nh))
+                max_free=0)  # 0: nu*N, every contact schedule (overflow to the workgroup kernel)
 
 
 def to_struct(p: dict):

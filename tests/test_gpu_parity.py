@@ -359,9 +359,11 @@ def test_pair_kernel_matches_single_and_oracle(gpu, orc, monkeypatch):
     """Two QPs per wavefront (csrc/mpc_pair.hpp, nf <= 30) against the one-QP-per-wave kernel
     (MPCQP_PAIR=0) and the oracle: odd batch (the last wave's upper half is idle), contact
     masks with fewer stance forces (nf < 30, uneven iteration counts inside a wave) and with
-    both feet down at one step (nf > max_free -> BAD_DIMS beside a solved neighbour)."""
+    both feet down at one step (nf > max_free -> BAD_DIMS beside a solved neighbour; the
+    context is capped at 30 free forces, so nothing overflows to the workgroup kernel)."""
     import mpcqp
     p = mpcqp.model_params("B")
+    p["max_free"] = 30
     B = 333
     batch = mpcqp.make_batch(p, B, seed=7)
     ct = batch["contact"].astype(np.uint64).copy()
@@ -482,3 +484,85 @@ def test_friction_rows_mixed_contact_vs_oracle(gpu, orc):
     assert not bad, bad[:10]
     np.testing.assert_allclose(o["cost"], ref["cost"], rtol=1e-9, atol=1e-9)
     assert np.mean(o["iters"] == ref["iters"]) >= 0.99
+
+
+def _prefilled(eng, batch):
+    import torch
+    d = eng.upload(batch)
+    d["U"].fill_(float("nan"))
+    d["cost"].fill_(float("nan"))
+    d["status"].fill_(99)
+    d["iters"].fill_(-1)
+    torch.cuda.synchronize()
+    return d
+
+
+@pytest.mark.parametrize("config,B", [("B", 512), ("C", 384)])
+def test_overflow_workgroup_kernel_vs_oracle(gpu, orc, config, B):
+    """Every contact schedule (qpOASES takes the dense nV = NU*N problem
+    whatever the bounds, src/QPSolver.cpp:87-96): alternating, double-support and standing
+    candidates (gait "mixed") plus random extra double-support and flight steps.  Instances
+    beyond the one-wave kernel's capacity (30 free forces for the paired kernel at N = 10, 64
+    for k_mpc at N = 20) go through the overflow list to the 4-wave workgroup kernel (up to 6N
+    = 60 / 120 free forces); every instance is written exactly once (sentinel pre-fill) and
+    matches the oracle."""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params(config)
+    batch = mpcqp.make_batch(p, B, seed=41, gait="mixed")
+    ct = batch["contact"].astype(np.uint64).copy()
+    rng = np.random.default_rng(43)
+    for i in range(B):
+        if i % 3 == 1:
+            ct[i] |= np.uint64(3 << (2 * int(rng.integers(p["N"]))))   # double support
+        if i % 5 == 2:
+            ct[i] &= ~np.uint64(3 << (2 * int(rng.integers(p["N"]))))  # flight
+    batch["contact"] = ct
+    nfree = np.array([3 * bin(int(c)).count("1") for c in ct])
+    cap = 30 if config == "B" else 64
+    assert (nfree > cap).sum() > B // 5 and (nfree <= cap).sum() > B // 5
+    assert nfree.max() == 6 * p["N"]  # standing candidates
+    eng = BatchEngine(p)
+    d = _prefilled(eng, batch)
+    eng.solve(d)
+    eng.sync()
+    o = {k: d[k].cpu().numpy() for k in ("U", "cost", "status", "iters")}
+    eng.close()
+    ref = orc.srbm_batch(p, batch["x0"], batch["xref"], batch["lin"], ct)
+    assert np.all(ref["status"] == 0)
+    np.testing.assert_array_equal(o["status"], ref["status"])
+    assert np.all(np.isfinite(o["U"])) and np.all(o["iters"] >= 0)
+    bad = [i for i in range(B) if not u_close(o["U"][i], ref["U"][i])]
+    assert not bad, (bad[:10], nfree[bad[:10]])
+    np.testing.assert_allclose(o["cost"], ref["cost"], rtol=1e-9, atol=1e-9)
+    big = nfree > cap
+    assert np.mean(o["iters"][big] == ref["iters"][big]) >= 0.95
+
+
+def test_overflow_full_size_mixed_gait(gpu, orc):
+    """config C at batch 65,536 with the mixed gait (a quarter standing, nf = 120): every
+    instance solved and written once, repeated calls re-arm the overflow list (identical
+    results), a random sample matches the oracle"""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("C")
+    B = 65536
+    batch = mpcqp.make_batch(p, B, seed=47, gait="mixed")
+    eng = BatchEngine(p)
+    d = _prefilled(eng, batch)
+    eng.solve(d)
+    eng.sync()
+    U1 = d["U"].cpu().numpy().copy()
+    st = d["status"].cpu().numpy().copy()
+    it = d["iters"].cpu().numpy().copy()
+    eng.solve(d)
+    eng.sync()
+    U2 = d["U"].cpu().numpy()
+    eng.close()
+    assert np.all(st == 0) and np.all(it >= 0) and np.all(np.isfinite(U1))
+    np.testing.assert_array_equal(U1, U2)
+    idx = np.random.default_rng(6).choice(B, 160, replace=False)
+    sub = {k: batch[k][idx] for k in batch}
+    ref = orc.srbm_batch(p, sub["x0"], sub["xref"], sub["lin"], sub["contact"])
+    for j, i in enumerate(idx):
+        assert u_close(U1[i], ref["U"][j]), i
