@@ -25,6 +25,7 @@ struct FastKernels {
     size_t pair_lds = 0;
     const void *wg = nullptr;  // workgroup per QP for the overflow list (nf <= 6N)
     size_t wg_lds = 0;
+    int wg_threads = 0;
     const void *disc = nullptr, *cs = nullptr, *mpc = nullptr;
     size_t disc_lds = 0, cs_lds = 0, mpc_lds = 0;
     int nx = 0, nu = 0;

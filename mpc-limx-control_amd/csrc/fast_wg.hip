@@ -12,9 +12,10 @@ namespace {
 
 // one 4-wave workgroup per QP; list != nullptr: the overflow list, else the whole batch
 template <int NU, int N, int MODEL, bool FRIC, bool GEN, int NF>
-__global__ void __launch_bounds__(kWgThreads, (NF <= 64 ? 3 : 1)) k_mpc_wg(MpcArgs a, int *list) {
+__global__ void __launch_bounds__(WgShape<NF>::THREADS, (NF <= 64 ? 3 : 1))
+    k_mpc_wg(MpcArgs a, int *list, int *rearm) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_w[];
-    wg_mpc_grid<NU, N, MODEL, FRIC, GEN, NF>(a, list, smem_w);
+    wg_mpc_grid<NU, N, MODEL, FRIC, GEN, NF>(a, list, rearm, smem_w);
 }
 
 // explicit-input kernels only: calculateGait (the generated-input path) puts one foot down
@@ -23,6 +24,7 @@ template <int N, bool FRIC, int NF>
 void add_wg(FastKernels &k) {
     k.wg = (const void *)&k_mpc_wg<6, N, 0, FRIC, false, NF>;
     k.wg_lds = WgSrbmLayout<6, N, FRIC, NF>::lds_bytes;
+    k.wg_threads = WgShape<NF>::THREADS;
 }
 
 }  // namespace

@@ -10,10 +10,11 @@
 //     are half 0, waves 2-3 half 1) holds columns [h NF/2, (h+1) NF/2) of row r: first of H_FF
 //     (then L, right-looking Cholesky), then of J = L^-T Q.  NF/2 <= 64 doubles per thread.
 //   * Cholesky: step k publishes column k (and g_k) to LDS, one barrier, every thread updates
-//     its half-row.  The half that owns column k keeps its live columns at the front of its
-//     register array (each update writes column j+1's result into slot j), so the column
-//     published at step k is always slot 0: runtime loops, compile-time register indices.
-//     L is parked in LDS (column-major packed) and g rides along (t = L^-1 g).
+//     its part of row r.  For the factorisation the columns are interleaved over the halves
+//     (even columns in half 0, odd in half 1), so after each pair of steps both halves drop
+//     their first slot together: the published column is always slot 0 (runtime loop,
+//     compile-time register indices).  L is parked in LDS (column-major packed) and g rides
+//     along (t = L^-1 g).
 //   * J = L^-T by back substitution of L' J = I, one row per step: the owner of row l scales
 //     and publishes it, every row r < l subtracts L(l, r) times it.  The two halves are
 //     independent here (each column of J is its own system).
@@ -31,8 +32,13 @@
 
 namespace mpcqp {
 
-constexpr int kWgRows = 128;             // rows per column half (two waves)
-constexpr int kWgThreads = 2 * kWgRows;  // four waves
+// rows per column half: one wave for NF <= 64, two waves for NF <= 128
+template <int NF>
+struct WgShape {
+    static constexpr int RW = NF <= 64 ? 64 : 128;
+    static constexpr int THREADS = 2 * RW;  // two or four waves
+    static constexpr int NWH = RW / 64;      // waves per half
+};
 
 // column k of the parked L, rows k..NF-1 (column-major packed, no padding)
 template <int NF>
@@ -40,28 +46,29 @@ __device__ __forceinline__ int wg_lcol(int k) { return k * NF - (k * (k - 1)) / 
 
 template <int NF>
 struct WgLayout {
-    static_assert(NF % 2 == 0 && NF >= 2 && NF <= kWgRows, "two column halves of <= 64");
-    static constexpr int NH = NF / 2;
+    static_assert(NF % 2 == 0 && NF >= 2 && NF <= 128, "two column halves of <= 64");
+    static constexpr int NH = NF / 2, RW = WgShape<NF>::RW;
     static constexpr int NRP = NF * (NF + 3) / 2;    // packed L, then packed R (roff)
-    static constexpr int CBW = kWgRows + 2;          // column broadcast: 128 rows + g slot
+    static constexpr int CBW = RW + 2;               // column broadcast: RW rows + g slot
     static constexpr int oL = 0;
     static constexpr int oCol = (NRP + 1) & ~1;      // [2][CBW]; then the rotations (2 NF)
     static constexpr int oD = oCol + 2 * CBW;        // d = J' n (published rows)
-    static constexpr int oDq = oD + kWgRows;         // d masked to c >= q, then the reflector v
-    static constexpr int oD2 = oDq + kWgRows;        // second friction row; drop carry
-    static constexpr int oPart = oD2 + kWgRows;      // [2][128] per-half partial sums
-    static constexpr int oT = oPart + 2 * kWgRows;   // t = L^-1 g; drop carry
-    static constexpr int oRinv = oT + kWgRows;       // 1/L(k,k), then 1/R(j,j)
-    static constexpr int oUs = oRinv + kWgRows;      // slot multipliers u
-    static constexpr int oRed = oUs + kWgRows;       // reduction slots
+    static constexpr int oDq = oD + RW;              // d masked to c >= q, then the reflector v
+    static constexpr int oD2 = oDq + RW;             // second friction row; drop carry
+    static constexpr int oPart = oD2 + RW;           // [2][RW] per-half partial sums
+    static constexpr int oT = oPart + 2 * RW;        // t = L^-1 g; drop carry
+    static constexpr int oRinv = oT + RW;            // 1/L(k,k), then 1/R(j,j)
+    static constexpr int oUs = oRinv + RW;           // slot multipliers u
+    static constexpr int oRed = oUs + RW;            // reduction slots
     static constexpr int oAct = oRed + 32;           // slot constraint ids (int)
-    static constexpr int doubles = oAct + kWgRows / 2;
+    static constexpr int doubles = oAct + RW / 2;
     static_assert(2 * CBW >= 2 * NF, "rotations fit the column buffers");
 };
 
 struct WgIds {
     int tid, h, r, wv, ln;
 };
+template <int RW>
 __device__ __forceinline__ WgIds wg_ids() {
     WgIds t;
     t.tid = (int)threadIdx.x;
@@ -71,34 +78,41 @@ __device__ __forceinline__ WgIds wg_ids() {
     asm volatile("" : "+v"(t.tid));
     // the half and the wave index are wave-uniform: in SGPRs, so the per-column LDS addresses
     // and masks of the unrolled loops are scalar (not a VGPR per column held across the loop)
-    t.h = __builtin_amdgcn_readfirstlane(t.tid >> 7);
-    t.r = t.tid & (kWgRows - 1);
+    t.h = __builtin_amdgcn_readfirstlane(t.tid / RW);
+    t.r = t.tid & (RW - 1);
     t.wv = __builtin_amdgcn_readfirstlane(t.tid >> 6);
     t.ln = lane();
     return t;
 }
 
-// lexicographic (value, id) minimum of the two half-0 wave results in red[o..o+3]
-__device__ __forceinline__ void wg_pick2(const double *red, int o, double &v, int &id) {
-    const double v0 = red[o], v1 = red[o + 2];
-    const int i0 = (int)red[o + 1], i1 = (int)red[o + 3];
-    const bool take1 = v1 < v0 || (v1 == v0 && i1 < i0);
-    v = take1 ? v1 : v0;
-    id = take1 ? i1 : i0;
+// lexicographic (value, id) minimum of the NWH half-0 wave results in red[o..o+2 NWH)
+template <int NWH>
+__device__ __forceinline__ void wg_pick(const double *red, int o, double &v, int &id) {
+    v = red[o];
+    id = (int)red[o + 1];
+    if constexpr (NWH == 2) {
+        const double v1 = red[o + 2];
+        const int i1 = (int)red[o + 3];
+        const bool take1 = v1 < v || (v1 == v && i1 < id);
+        v = take1 ? v1 : v;
+        id = take1 ? i1 : id;
+    }
 }
 
-// hr: thread (r, h) holds H_FF(r, h NF/2 + j) for c <= r (rows / columns >= nf padded with the
-// identity, so every step runs unpredicated; entries above the diagonal are never read).
+// hr: thread (r, h) holds H_FF(r, 2 j + h) for c <= r (columns interleaved over the halves;
+// rows / columns >= nf padded with the identity, so every step runs unpredicated; entries
+// above the diagonal are never read).
 // g: g_r on both halves of row r (0 beyond nf).  W: WgLayout<NF>::doubles of LDS.
 // C.L must provide xs (128), cb, st, fid, pos, xfull.  Fills C.{status, x, fval, q, iters};
 // every thread returns x_r of its row.
 template <int NF>
 __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double g, double *W) {
     using Lay = WgLayout<NF>;
-    constexpr int NH = Lay::NH, CBW = Lay::CBW;
+    constexpr int NH = Lay::NH, CBW = Lay::CBW, RW = Lay::RW, NWH = WgShape<NF>::NWH;
+    constexpr bool TWO = RW > 64;  // wave 0 keeps two slots per lane (ln, ln + 64)
     GiLds &L = C.L;
     const SolveProblem &P = *C.P;
-    const WgIds T = wg_ids();
+    const WgIds T = wg_ids<RW>();
     const int h = T.h, r = T.r, wv = T.wv, ln = T.ln, tid = T.tid;
     const int nf = C.nf, mt = C.mt;
     int status = C.status;
@@ -111,47 +125,60 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
     double x = 0.0, fval = 0.0;
     int iters = 0, q = 0;
     double Jr[NH];
+    MPCQP_STAMP_INIT(tst);
 
     // ---- Cholesky H_FF = L L' (right-looking) with the forward solve L t = g in the same sweep
     double gv = (live && r < nf) ? g : 0.0;
     if (status == ST_OK && nf > 0) {
         bool bad = false;
-        for (int k = 0; k < nf; ++k) {
-            const int kh = k >= NH ? 1 : 0;
-            double *cb = colb + (k & 1) * CBW;
-            if (h == kh && live && r >= k) cb[r] = hr[0];  // column k (pivot at r == k)
-            if (tid == k) cb[kWgRows] = gv;                 // g_k (thread (k, 0))
-            __syncthreads();
-            const double piv = cb[k];
-            bad |= !(piv > 0.0);
-            const double isq = rsqrt_nr(piv);                // 1 / L(k,k)
-            const double hk = (live && r > k) ? cb[r] : 0.0; // H(r, k)
-            const double lr = hk * isq;                      // L(r, k)
-            const double tk = cb[kWgRows] * isq;             // t_k
-            gv = (r == k) ? tk : ((r > k) ? gv - lr * tk : gv);
-            if (h == kh && live && r >= k) Lc[wg_lcol<NF>(k) + r - k] = (r == k) ? piv * isq : lr;
-            if (tid == 0) rinv[k] = isq;
-            const double fr = hk * (isq * isq);              // L(r,k) / L(k,k)
-            if (h == kh) {
-                // this half owns column k: column k+1+j moves into slot j
-                const double *src = cb + k + 1;
+        // Columns are interleaved over the halves for the factorisation (hr[j] of half h is
+        // column 2(m + j) + h after m super-steps): super-step m eliminates column 2m (owned
+        // by half 0, its slot 0) and then column 2m + 1 (half 1, slot 0), after which both
+        // halves shift their arrays by one.  Both halves run the same straight-line code, the
+        // published column is always slot 0 (compile-time register indices, runtime loop).
+        const int npair = (nf + 1) >> 1;
+        for (int m = 0; m < npair; ++m) {
 #pragma unroll
-                for (int j = 0; j < NH - 1; ++j) {
-                    hr[j] = hr[j + 1] - fr * src[j];
-                    if ((j & 7) == 7) step_fence();  // bound the loads in flight
-                }
-                hr[NH - 1] = 0.0;
-            } else if (h > kh) {
-                const double *src = cb + NH;
+            for (int e = 0; e < 2; ++e) {
+                const int k = 2 * m + e;
+                if (k >= nf) break;
+                double *cb = colb + e * CBW;
+                if (h == e && live && r >= k) cb[r] = hr[0];   // column k (pivot at r == k)
+                if (tid == k) cb[RW] = gv;                      // g_k (thread (k, 0))
+                __syncthreads();
+                const double piv = cb[k];
+                bad |= !(piv > 0.0);
+                const double isq = rsqrt_nr(piv);               // 1 / L(k,k)
+                const double hk = (live && r > k) ? cb[r] : 0.0; // H(r, k)
+                const double lr = hk * isq;                     // L(r, k)
+                const double tk = cb[RW] * isq;                 // t_k
+                gv = (r == k) ? tk : ((r > k) ? gv - lr * tk : gv);
+                if (h == e && live && r >= k) Lc[wg_lcol<NF>(k) + r - k] = (r == k) ? piv * isq : lr;
+                if (tid == 0) rinv[k] = isq;
+                const double fr = hk * (isq * isq);             // L(r,k) / L(k,k)
+                if (e == 0) {
+                    // slot j = column 2(m + j) + h
+                    const double *src = cb + 2 * m + h;
 #pragma unroll
-                for (int j = 0; j < NH; ++j) {
-                    hr[j] -= fr * src[j];
-                    if ((j & 7) == 7) step_fence();
+                    for (int j = 0; j < NH; ++j) {
+                        hr[j] -= fr * src[2 * j];
+                        if ((j & 7) == 7) step_fence();  // bound the loads in flight
+                    }
+                } else {
+                    // the update of column 2(m + j + 1) + h lands in slot j: both slots 0 done
+                    const double *src = cb + 2 * (m + 1) + h;
+#pragma unroll
+                    for (int j = 0; j < NH - 1; ++j) {
+                        hr[j] = hr[j + 1] - fr * src[2 * j];
+                        if ((j & 7) == 7) step_fence();
+                    }
+                    hr[NH - 1] = 0.0;
                 }
             }
         }
         if (bad) status = ST_NOT_PD;
     }
+    MPCQP_STAMP(C.stamps, 5, tst);
     MPCQP_CUT(C.cut, 4);
 
     if (status == ST_OK && nf > 0) {
@@ -180,6 +207,7 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
                 }
             }
         }
+        MPCQP_STAMP(C.stamps, 6, tst);
         MPCQP_CUT(C.cut, 5);
         // ---- unconstrained minimum x = -J t, objective -|t|^2 / 2
         double s4[4] = {0.0, 0.0, 0.0, 0.0};
@@ -189,17 +217,18 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             s4[j & 3] += Jr[j] * tb[j];
             if ((j & 7) == 7) step_fence();
         }
-        part[h * kWgRows + r] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+        part[h * RW + r] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
         if (h == 0) {
             const double tt = wave_sum((r < nf) ? gv * gv : 0.0);
             if (ln == 0) red[wv] = tt;
         }
         __syncthreads();
-        x = (r < nf) ? -(part[r] + part[kWgRows + r]) : 0.0;
-        fval = -0.5 * (red[0] + red[1]);
+        x = (r < nf) ? -(part[r] + part[RW + r]) : 0.0;
+        fval = -0.5 * (NWH == 2 ? red[0] + red[1] : red[0]);
         if (h == 0) L.xs[r] = x;
         __syncthreads();
     }
+    MPCQP_STAMP(C.stamps, 7, tst);
     MPCQP_CUT(C.cut, 6);
 
     // ---- dual active-set loop: one pass = one add or drop step
@@ -244,7 +273,7 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             wave_argmin(best, bid);
             if (h == 0 && ln == 0) { red[4 + 2 * wv] = best; red[5 + 2 * wv] = (double)bid; }
             __syncthreads();
-            wg_pick2(red, 4, best, bid);
+            wg_pick<NWH>(red, 4, best, bid);
             if (bid == 0x7fffffff) break;  // optimal
             p = bid;
             if (tid == 0) us[q] = 0.0;
@@ -314,7 +343,7 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
                 z4[j & 3] += Jr[j] * dq[j];
                 if ((j & 7) == 7) step_fence();
             }
-            part[h * kWgRows + r] = (z4[0] + z4[1]) + (z4[2] + z4[3]);
+            part[h * RW + r] = (z4[0] + z4[1]) + (z4[2] + z4[3]);
         }
         if (h == 0) {  // |d|^2, |d2|^2, |d2|^2 without d_q: thread r owns d_r
             const double dv = (r < nf) ? dB[r] : 0.0;
@@ -325,19 +354,21 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
         double r0 = 0.0, r1 = 0.0;  // wave 0: r of slots ln and ln + 64
         if (wv == 0 && q > 0) {
             // r = R^-1 d(0:q), back substitution (R packed in LDS, 1/R(j,j) beside it)
-            double v0 = (ln < q) ? dB[ln] : 0.0, v1 = (ln + 64 < q) ? dB[ln + 64] : 0.0;
+            double v0 = (ln < q) ? dB[ln] : 0.0, v1 = (TWO && ln + 64 < q) ? dB[ln + 64] : 0.0;
             int j = q - 1;
             double ra = (ln < j) ? Lc[roff(j) + ln] : 0.0;
-            double rb = (ln + 64 < j) ? Lc[roff(j) + ln + 64] : 0.0;
+            double rb = (TWO && ln + 64 < j) ? Lc[roff(j) + ln + 64] : 0.0;
             for (; j >= 0; --j) {
                 // prefetch column j - 1 while column j is applied
                 const double na = (j > 0 && ln < j - 1) ? Lc[roff(j - 1) + ln] : 0.0;
-                const double nb = (j > 0 && ln + 64 < j - 1) ? Lc[roff(j - 1) + ln + 64] : 0.0;
+                const double nb = (TWO && j > 0 && ln + 64 < j - 1) ? Lc[roff(j - 1) + ln + 64] : 0.0;
                 const double rj = (j < 64 ? readlane(v0, j) : readlane(v1, j - 64)) * rinv[j];
                 if (ln == j) r0 = rj;
-                if (ln + 64 == j) r1 = rj;
                 if (ln < j) v0 -= ra * rj;
-                if (ln + 64 < j) v1 -= rb * rj;
+                if constexpr (TWO) {
+                    if (ln + 64 == j) r1 = rj;
+                    if (ln + 64 < j) v1 -= rb * rj;
+                }
                 ra = na;
                 rb = nb;
             }
@@ -345,7 +376,7 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             double t1 = INFINITY;
             int ks = 0x7fffffff;
             if (ln < q && r0 > kRTol * rmax) { t1 = us[ln] / r0; ks = ln; }
-            if (ln + 64 < q && r1 > kRTol * rmax) {
+            if (TWO && ln + 64 < q && r1 > kRTol * rmax) {
                 const double tt = us[ln + 64] / r1;
                 if (tt < t1) { t1 = tt; ks = ln + 64; }
             }
@@ -353,8 +384,10 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             if (ln == 0) { red[16] = t1; red[17] = (double)ks; }
         }
         __syncthreads();
-        const double z = part[r] + part[kWgRows + r];
-        const double dd = red[8] + red[11], zn = red[9] + red[12], zq = red[10] + red[13];
+        const double z = part[r] + part[RW + r];
+        const double dd = NWH == 2 ? red[8] + red[11] : red[8];
+        const double zn = NWH == 2 ? red[9] + red[12] : red[9];
+        const double zq = NWH == 2 ? red[10] + red[13] : red[10];
         double t1 = INFINITY;
         int kslot = 0x7fffffff;
         if (q > 0) { t1 = red[16]; kslot = (int)red[17]; }
@@ -368,13 +401,16 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             fval += t * zn * (0.5 * t + uq);
         }
         if (wv == 0) {
-            double u0 = us[ln], u1 = us[ln + 64];
+            double u0 = us[ln];
             if (ln < q) u0 -= t * r0;
             if (ln == q) u0 += t;
-            if (ln + 64 < q) u1 -= t * r1;
-            if (ln + 64 == q) u1 += t;
             us[ln] = u0;
-            us[ln + 64] = u1;
+            if constexpr (TWO) {
+                double u1 = us[ln + 64];
+                if (ln + 64 < q) u1 -= t * r1;
+                if (ln + 64 == q) u1 += t;
+                us[ln + 64] = u1;
+            }
         }
         const bool add = !isinf(t2) && t2 <= t1;
         if (add) {
@@ -389,7 +425,7 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             }
             if (wv == 0) {
                 if (ln < q) Lc[roff(q) + ln] = dB[ln];
-                if (ln + 64 < q) Lc[roff(q) + ln + 64] = dB[ln + 64];
+                if (TWO && ln + 64 < q) Lc[roff(q) + ln + 64] = dB[ln + 64];
                 if (ln == 0) {
                     Lc[roff(q) + q] = rqq;
                     rinv[q] = 1.0 / rqq;
@@ -409,9 +445,9 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
                     w4[j & 3] += Jr[j] * v[j];
                     if ((j & 7) == 7) step_fence();
                 }
-                part[h * kWgRows + r] = (w4[0] + w4[1]) + (w4[2] + w4[3]);
+                part[h * RW + r] = (w4[0] + w4[1]) + (w4[2] + w4[3]);
                 __syncthreads();
-                const double f = beta * (part[r] + part[kWgRows + r]);
+                const double f = beta * (part[r] + part[RW + r]);
 #pragma unroll
                 for (int j = 0; j < NH; ++j) {
                     Jr[j] -= f * v[j];
@@ -424,17 +460,21 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             const int k = kslot;
             if (wv == 0) {
                 const int dropped = acts[k];
-                const double un0 = us[ln + 1], un1 = (ln + 65 < kWgRows) ? us[ln + 65] : 0.0;
-                const int an0 = acts[ln + 1], an1 = (ln + 65 < kWgRows) ? acts[ln + 65] : 0;
+                const double un0 = (ln + 1 < RW) ? us[ln + 1] : 0.0;
+                const int an0 = (ln + 1 < RW) ? acts[ln + 1] : 0;
+                const double un1 = (TWO && ln + 65 < RW) ? us[ln + 65] : 0.0;
+                const int an1 = (TWO && ln + 65 < RW) ? acts[ln + 65] : 0;
                 wave_sync();
-                if (ln >= k && ln < q - 1) { us[ln] = un0; acts[ln] = an0; }
-                if (ln + 64 >= k && ln + 64 < q - 1) { us[ln + 64] = un1; acts[ln + 64] = an1; }
+                // slots k .. q-1 take their successor's entries; slot q-1 receives slot q's
+                // u, the partial multiplier of the constraint being added
+                if (ln >= k && ln < q) { us[ln] = un0; acts[ln] = an0; }
+                if (TWO && ln + 64 >= k && ln + 64 < q) { us[ln + 64] = un1; acts[ln + 64] = an1; }
                 if (ln == 0) L.st[dropped] = 1;
                 for (int j = k; j < q - 1; ++j) {
                     const double v0 = (ln <= j + 1) ? Lc[roff(j + 1) + ln] : 0.0;
-                    const double v1 = (ln + 64 <= j + 1) ? Lc[roff(j + 1) + ln + 64] : 0.0;
+                    const double v1 = (TWO && ln + 64 <= j + 1) ? Lc[roff(j + 1) + ln + 64] : 0.0;
                     if (ln <= j + 1) Lc[roff(j) + ln] = v0;
-                    if (ln + 64 <= j + 1) Lc[roff(j) + ln + 64] = v1;
+                    if (TWO && ln + 64 <= j + 1) Lc[roff(j) + ln + 64] = v1;
                 }
                 const int qn = q - 1;
                 for (int j = ln; j < NF; j += kWave) { rot[2 * j] = 1.0; rot[2 * j + 1] = 0.0; }
@@ -446,7 +486,7 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
                         const double ih = 1.0 / hh;
                         const double c = a_ * ih, s_ = bb * ih;
 #pragma unroll
-                        for (int o = 0; o < 2; ++o) {
+                        for (int o = 0; o < (TWO ? 2 : 1); ++o) {
                             const int l = j + 1 + ln + 64 * o;
                             if (l < qn) {
                                 const double y0 = Lc[roff(l) + j], y1 = Lc[roff(l) + j + 1];
@@ -500,6 +540,7 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
         }
         __syncthreads();
     }
+    MPCQP_STAMP(C.stamps, 8, tst);
     MPCQP_CUT(C.cut, 7);
     C.status = status;
     C.x = x;
@@ -512,13 +553,15 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
 
 // outputs of a workgroup solve: x of the free variables from the rows of half 0, fixed values,
 // cost / status / iterations (gi_write's conventions)
+template <int NF>
 __device__ __forceinline__ void gi_write_wg(GiCtx &C, const SolveOut &O) {
+    constexpr int RW = WgShape<NF>::RW;
     const SolveProblem &P = *C.P;
     GiLds &L = C.L;
-    const WgIds T = wg_ids();
+    const WgIds T = wg_ids<RW>();
     const int nV = P.nV, nf = C.nf;
     const bool have_map = nf <= C.nfmax;
-    for (int v = T.tid; v < nV; v += kWgThreads) {
+    for (int v = T.tid; v < nV; v += 2 * RW) {
         const int pv = L.pos[v];
         if (pv < 0 || !have_map) O.x[v] = (pv < 0) ? L.xfull[v] : 0.0;
     }

@@ -52,7 +52,7 @@ struct MpcArgs {
     int *ovf;  // overflow list (mpc_wg.hpp) for instances beyond the kernel's free capacity
 };
 
-// overflow list layout (int): [0] count, [1] exit ticket, [2 ..] instance ids
+// overflow list layout (int): [0] count, [1] unused, [2 ..] instance ids
 constexpr int kListHead = 2;
 __device__ __forceinline__ void wg_list_append(int *list, int b) {
     const int i = __hip_atomic_fetch_add(&list[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

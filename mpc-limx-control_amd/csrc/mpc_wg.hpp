@@ -1,7 +1,7 @@
 // mpc_wg.hpp -- the fused per-tick step (mpc_fused.hpp) for instances with more free forces
 // than the one-wave kernels hold: up to NF = 64 at N = 10 and NF = 128 at N = 20, i.e. every
-// contact schedule including double support and standing (nf = 6 N).  One 4-wave workgroup
-// per QP: wave 0 runs the same input / model / condensed-term phases as fast_mpc, every thread
+// contact schedule including double support and standing (nf = 6 N).  One workgroup (2 waves for
+// NF <= 64, 4 above) per QP: wave 0 runs the same input / model / condensed-term phases as fast_mpc, every thread
 // then builds its half-row of H_FF from the closed form and gi_run_wg (gi_wg.hpp) solves.
 //
 // Reference: mpcQP::mpcQP + buildSystemModel (include/mpcQP.h:35-119, 121-182),
@@ -26,7 +26,7 @@ struct WgSrbmLayout {
     static constexpr int MT = 2 * NF + NFRIC;
     // live for the whole solve: x mirror (one per row), fixed values, the bounds' b
     static constexpr int oXS = 0;
-    static constexpr int oXF = oXS + kWgRows;
+    static constexpr int oXF = oXS + WgShape<NF>::RW;
     static constexpr int oMisc = oXF + NV;                 // nf and status for waves 1-3
     static constexpr int oCB = oMisc + 2;
     static constexpr int oU = (oCB + 2 * NF + 1) & ~1;     // shared region (16-B aligned)
@@ -54,7 +54,7 @@ template <int NU, int N, int MODEL, bool FRIC, bool GEN, int NF>
 __device__ __forceinline__ void wg_mpc_one(const MpcArgs &a, int b, unsigned char *smem) {
     using Lay = WgSrbmLayout<NU, N, FRIC, NF>;
     constexpr int NV = Lay::NV, NH = NF / 2;
-    const WgIds T = wg_ids();
+    const WgIds T = wg_ids<WgShape<NF>::RW>();
     double *D = reinterpret_cast<double *>(smem);
 
     SolveProblem P;
@@ -72,8 +72,9 @@ __device__ __forceinline__ void wg_mpc_one(const MpcArgs &a, int b, unsigned cha
     P.max_iter = a.max_iter;
     GiCtx C;
     C.wide = 1;
-    C.stamps = nullptr;
+    C.stamps = a.stamps;
     C.cut = 0;
+    MPCQP_STAMP_INIT(tst);
     C.P = &P;
     C.nfmax = NF;
     C.L.ld = NF | 1;
@@ -108,6 +109,7 @@ __device__ __forceinline__ void wg_mpc_one(const MpcArgs &a, int b, unsigned cha
     C.nfric = FRIC ? 4 * N * 2 : 0;
     C.mt = 2 * C.nf + C.nfric;
     C.c0 = 0.0;
+    MPCQP_STAMP(a.stamps, 0, tst);
 
     // ---- H_FF half-rows (lower triangle; identity padding beyond nf) and g
     const int nf = C.nf, r = T.r, h = T.h;
@@ -118,30 +120,36 @@ __device__ __forceinline__ void wg_mpc_one(const MpcArgs &a, int b, unsigned cha
         const int vi = C.L.fid[r];
 #pragma unroll
         for (int j = 0; j < NH; ++j) {
-            const int c = h * NH + j;
+            const int c = 2 * j + h;  // interleaved columns (gi_run_wg's factorisation layout)
             hr[j] = (c < nf && c <= r) ? mpc_h_entry<Lay, NU, N>(D, vi, C.L.fid[c]) : 0.0;
             step_fence();  // one entry at a time (the entries share no work)
         }
         g = mpc_g_entry<Lay, NU, N>(D, vi);
     } else {
 #pragma unroll
-        for (int j = 0; j < NH; ++j) hr[j] = (r == h * NH + j) ? 1.0 : 0.0;
+        for (int j = 0; j < NH; ++j) hr[j] = (r == 2 * j + h) ? 1.0 : 0.0;
     }
     __syncthreads();  // the solver's workspace overlays the condensed terms
+    MPCQP_STAMP(a.stamps, 3, tst);
     gi_run_wg<NF>(C, hr, g, D + Lay::oW);
+    MPCQP_STAMP_INIT(tw);
     SolveOut O;
     O.x = a.U + (size_t)b * NV;
     O.cost = a.cost + b;
     O.status = a.status + b;
     O.iters = a.iters + b;
     O.y = nullptr;
-    gi_write_wg(C, O);
+    gi_write_wg<NF>(C, O);
+    MPCQP_STAMP(a.stamps, 9, tw);
 }
 
-// list == nullptr: instance b = blockIdx.x (+ grid stride) of the whole batch; otherwise the
-// instances of the overflow list, and the last workgroup out re-arms the list
+// list == nullptr: instance b = blockIdx.x (+ grid stride) of the whole batch.  Otherwise the
+// instances of the overflow list the one-wave kernel just filled; the context alternates two
+// lists, and this launch re-arms the other one (its last reader was the previous launch, its
+// next writer the next one-wave launch), so no exit ticket is needed.
 template <int NU, int N, int MODEL, bool FRIC, bool GEN, int NF>
-__device__ __forceinline__ void wg_mpc_grid(const MpcArgs &a, int *list, unsigned char *smem) {
+__device__ __forceinline__ void wg_mpc_grid(const MpcArgs &a, int *list, int *rearm,
+                                            unsigned char *smem) {
     if (!list) {
         for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
             wg_mpc_one<NU, N, MODEL, FRIC, GEN, NF>(a, b, smem);
@@ -149,17 +157,12 @@ __device__ __forceinline__ void wg_mpc_grid(const MpcArgs &a, int *list, unsigne
         }
         return;
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(rearm, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int count = __hip_atomic_load(&list[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int i = blockIdx.x; i < count; i += gridDim.x) {
         wg_mpc_one<NU, N, MODEL, FRIC, GEN, NF>(a, list[kListHead + i], smem);
         __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        const int t = __hip_atomic_fetch_add(&list[1], 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (t == (int)gridDim.x - 1) {  // every workgroup has read the count: re-arm
-            __hip_atomic_store(&list[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&list[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
 }
 

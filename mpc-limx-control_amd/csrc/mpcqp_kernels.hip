@@ -518,8 +518,9 @@ struct mpcqp_ctx {
     size_t ab_cap = 0;
     unsigned long long *dstamps = nullptr;  // diagnostic phase cycles (stamps build)
     unsigned long long *dsel = nullptr;     // k_select_min: per-block partial keys + ticket
-    int *dlist = nullptr;                   // overflow list [count, ticket, ids...] (mpc_wg.hpp)
-    size_t list_cap = 0;                    // instances the list holds
+    int *dlist = nullptr;                   // two overflow lists [count, -, ids...] (mpc_wg.hpp)
+    size_t list_cap = 0;                    // instances a list holds
+    int list_par = 0;                       // the list the next launch fills
     int wg_grid = 0;                        // resident workgroups of the workgroup kernel
     // host-pointer entry point staging
     void *hbuf = nullptr;
@@ -811,7 +812,7 @@ int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
         int dev_cus = 0, nb = 0;
         hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, device);
         set_lds(c->fk.wg, c->fk.wg_lds);
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, c->fk.wg, kWgThreads, c->fk.wg_lds);
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, c->fk.wg, c->fk.wg_threads, c->fk.wg_lds);
         c->wg_grid = std::max(1, nb) * std::max(1, dev_cus);
     }
     c->m.Q = c->m.R = c->m.P = nullptr;  // host pointers are not kept
@@ -989,10 +990,13 @@ static int ensure_list(mpcqp_ctx *c, int B) {
     hipFree(c->dlist);
     c->dlist = nullptr;
     c->list_cap = 0;
-    if (hipMalloc(&c->dlist, sizeof(int) * (kListHead + (size_t)B)) != hipSuccess ||
-        hipMemsetAsync(c->dlist, 0, sizeof(int) * kListHead, c->stream) != hipSuccess)
+    const size_t stride = kListHead + (size_t)B;
+    if (hipMalloc(&c->dlist, sizeof(int) * 2 * stride) != hipSuccess ||
+        hipMemsetAsync(c->dlist, 0, sizeof(int) * kListHead, c->stream) != hipSuccess ||
+        hipMemsetAsync(c->dlist + stride, 0, sizeof(int) * kListHead, c->stream) != hipSuccess)
         return MPCQP_ERR_DEVICE;
     c->list_cap = B;
+    c->list_par = 0;
     return MPCQP_OK;
 }
 
@@ -1001,20 +1005,25 @@ static int ensure_list(mpcqp_ctx *c, int B) {
 // kernel, launched right after on the same stream
 static int launch_mpc(mpcqp_ctx *c, bool gen, int B, MpcArgs *a) {
     a->ovf = nullptr;
+    int *list = nullptr, *rearm = nullptr;
     if (c->fk.wg && !gen) {
         const int rc = ensure_list(c, B);
         if (rc) return rc;
-        a->ovf = c->dlist;
+        const size_t stride = kListHead + c->list_cap;
+        list = c->dlist + (c->list_par ? stride : 0);
+        rearm = c->dlist + (c->list_par ? 0 : stride);
+        a->ovf = list;
     }
     const void *pk = gen ? c->fk.pair_gen : c->fk.pair;
     int rc = pk ? launch(pk, (B + 1) / 2, c->fk.pair_lds, c->stream, a)
                 : launch(gen ? c->fk.mpc_gen : c->fk.mpc, B, c->fk.mpc_lds, c->stream, a);
     if (rc || !a->ovf) return rc;
-    int *list = c->dlist;
-    void *args[] = {a, &list};
+    void *args[] = {a, &list, &rearm};
     const int grid = std::max(1, std::min(B, c->wg_grid));
-    return hip_status(hipLaunchKernel(c->fk.wg, dim3(grid), dim3(kWgThreads), args, c->fk.wg_lds,
-                                      c->stream));
+    rc = hip_status(hipLaunchKernel(c->fk.wg, dim3(grid), dim3(c->fk.wg_threads), args, c->fk.wg_lds,
+                                    c->stream));
+    c->list_par ^= 1;
+    return rc;
 }
 
 int mpcqp_batch_condense(mpcqp_ctx *c, int B, const double *x0, const double *xref,

@@ -22,13 +22,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="B")
     ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--gait", default="alternating", help="make_batch gait (GAITS)")
     args = ap.parse_args()
     import mpcqp
     from mpcqp._lib import lib
     from mpcqp.engine import BatchEngine
     p = mpcqp.model_params(args.config)
     eng = BatchEngine(p)
-    d = eng.upload(mpcqp.make_batch(p, args.batch))
+    d = eng.upload(mpcqp.make_batch(p, args.batch, gait=args.gait))
     buf = (C.c_uint64 * 16)()
     assert lib().mpcqp_debug_phase_cycles(eng.ctx, buf, 16) == 0, "not the stamps build"
     eng.solve(d)
@@ -39,7 +40,7 @@ def main():
     assert lib().mpcqp_debug_phase_cycles(eng.ctx, buf, 16) == 0
     cyc = np.array(buf[:12], dtype=np.float64) / args.batch
     tot_cs = cyc[:10].sum()
-    print(f"config {args.config}, batch {args.batch}, mean iters "
+    print(f"config {args.config}, gait {args.gait}, batch {args.batch}, mean iters "
           f"{d['iters'].float().mean().item():.2f}; cycles per QP (wave-serial)")
     for i, n in enumerate(NAMES):
         share = cyc[i] / (tot_cs if i < 10 else cyc[10:12].sum())

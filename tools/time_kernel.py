@@ -12,14 +12,18 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--configs", default="B,C,L")
 ap.add_argument("--batch", type=int, default=65536)
 ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--gait", default="alternating")
+ap.add_argument("--max-free", type=int, default=None)
 args = ap.parse_args()
 import mpcqp  # noqa: E402
 from mpcqp.engine import BatchEngine  # noqa: E402
 print("lib", os.environ.get("MPCQP_LIB", "default"))
 for cfg in args.configs.split(","):
     p = mpcqp.model_params(cfg)
+    if args.max_free is not None:
+        p["max_free"] = args.max_free
     eng = BatchEngine(p)
-    d = eng.upload(mpcqp.make_batch(p, args.batch))
+    d = eng.upload(mpcqp.make_batch(p, args.batch, gait=args.gait))
     eng.enable_timing(True)
     ts = []
     for r in range(args.reps + 3):
