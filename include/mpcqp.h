@@ -115,6 +115,9 @@ int mpcqp_plant_step(int nx, int nu, const double *Ad, const double *Bd, double 
 /* ---- batched engine ------------------------------------------------------------------ */
 #define MPCQP_MODEL_SRBM 0    /* convex-MPC single rigid body, 13 states, 6 inputs (2 feet) */
 #define MPCQP_MODEL_LITERAL 1 /* reference mpcQP::buildSystemModel, 13 states, 3 inputs    */
+#define MPCQP_MODEL_DENSE 2   /* any continuous model given per instance ([Ac | Bc] in lin),
+                               * dense Q/R/P, input box u_min..u_max: the whole-body
+                               * linearisation (BASELINE config E, 24/6/16)                 */
 #define MPCQP_CONS_BOX 0      /* per-foot force box from the contact schedule              */
 #define MPCQP_CONS_FRICTION 1 /* box + linearised friction pyramid |fx|,|fy| <= mu fz      */
 
@@ -139,8 +142,10 @@ typedef struct mpcqp_model {
 /* Per-instance inputs (device pointers, instance-major = one contiguous record per QP):
  *   x0      [B][nx]          initial state  [rpy, p, omega, v, g]      (include/mpcQP.h:66-71)
  *   xref    [B][N+1][nx]     reference, column i = step i (Eigen col-major 13 x (N+1))
- *   lin     [B][8]           SRBM: {yaw, r_L xyz, r_R xyz, 0}; LITERAL: {dx, dy, dz, ...}
+ *   lin     [B][8]           SRBM: {yaw, r_L xyz, r_R xyz, 0}; LITERAL: {dx, dy, dz, ...};
+ *           [B][nx*(nx+nu)]  DENSE: [Ac | Bc] column-major (continuous time)
  *   contact [B]              uint64, bit 2k = left foot in contact at step k, 2k+1 = right
+ *                            (SRBM only; nullable otherwise)
  * Outputs (device pointers):
  *   U [B][nu*N] (column-major nu x N: U_opt.col(0) = first nu entries), cost [B],
  *   status [B] (MPCQP_* per instance), iters [B].                                          */

@@ -1,0 +1,272 @@
+// dense_wg.hpp -- the per-tick step for a DENSE continuous model (BASELINE config E: the
+// 24-state whole-body linearisation of TRON1, NU = 6 joint torques, N = 16), one 4-wave
+// workgroup per QP:
+//
+//   discretisation   [Ad | Bd] = top block of exp([[Ac, Bc], [0, 0]] Ts): Eigen's Pade degree
+//                    selection + scaling and squaring (wave_expm, condense.hpp)
+//                                                            QPSolver::discretizeSystem,
+//                                                            src/QPSolver.cpp:21-29
+//   condensing       H = 2 (B'QB + R), f = 2 B'Q (A x0 - xref)   QPSolver::buildQPParams,
+//                    src/QPSolver.cpp:31-81 -- the reference's dense (nx(N+1))^2 product is
+//                    restructured into genuinely dense NX x NX contractions on the FP64
+//                    matrix cores (mfma_ops.hpp):
+//                      Phi_a = Ad^a Bd                 (a = 0..N-1, by doubling: Ad^2, Ad^4 ..)
+//                      Z_{N-1} = P,  Z_i = Q + Ad' Z_{i+1} Ad      (backward recursion)
+//                      Y_i = Bd' Z_i,  H(i,j) = 2 (Y_i Phi_{i-j} + R [i == j])   (i >= j)
+//                    and f by the matching vector recursion s_i = W_{i+1} e_{i+1} + Ad' s_{i+1},
+//                    f_i = 2 Bd' s_i (e_m = Ad^m x0 - xref_m) on the VALU
+//   solve            box u_min <= u <= u_max (src/QPSolver.cpp:67-68), every input free:
+//                    gi_run_wg (gi_wg.hpp) on the NV = 96 free variables
+//
+// The H rows reach the solver's registers through 16-row tiles of M = [Y_0; ..; Y_{N-1}] Phi
+// staged in LDS (H(r, c) = 2 M(r, (k_r - k_c) NU + c mod NU)), so no NV x NV matrix is ever
+// stored.  Per instance: [Ac | Bc] (NX x NS), x0, xref in; U, cost, status, iterations out.
+#pragma once
+#include "condense.hpp"
+#include "gi_wg.hpp"
+#include "mfma_ops.hpp"
+#include "mpc_fused.hpp"
+
+namespace mpcqp {
+
+template <int NX, int NU, int N>
+struct DenseLayout {
+    static constexpr int NS = NX + NU, NV = NU * N, NF = NV;
+    static constexpr int RW = WgShape<NF>::RW;
+    static constexpr int LD = NX + 1;   // odd leading dimension of the NX-row operands
+    static constexpr int LY = NV + 1;   // the Y stack (NV x NX)
+    static constexpr int LS = 17;       // a staged 16-row tile of M (16 x NV)
+    static constexpr int MT = 2 * NF;
+    // live for the whole solve: x mirror, fixed values, misc (nf, status), the bounds' b
+    static constexpr int oXS = 0, oXF = oXS + RW, oMisc = oXF + NV, oCB = oMisc + 2;
+    static constexpr int oU = (oCB + 2 * NF + 1) & ~1;
+    // front: [Ad | Bd], x0, xref, f, then a region the phases take turns on
+    static constexpr int oAB = oU;
+    static constexpr int oX0 = oAB + NX * NS;
+    static constexpr int oXr = oX0 + NX;
+    static constexpr int oF = oXr + NX * (N + 1);
+    static constexpr int oR = (oF + NV + 1) & ~1;
+    //   discretisation view
+    static constexpr int oT = oR;                       // [Ac | Bc] Ts
+    static constexpr int oWs = oT + NX * NS;            // wave_expm scratch (7 NX NS)
+    static constexpr int nExpm = oWs + 7 * NX * NS - oR;
+    //   condensing view
+    static constexpr int oPhi = oR;                     // Phi_a, NX x NV (ld LD)
+    static constexpr int oPw = oPhi + LD * NV;          // 3 NX x NX (ld LD): powers, Z, Z', Z Ad
+    static constexpr int oY = oPw + 3 * LD * NX;        // Y stack, NV x NX (ld LY)
+    static constexpr int oXf = oY + LY * NX;            // e_m = Ad^m x0 - xref_m, NX x (N+1)
+    static constexpr int oSv = oXf + NX * (N + 1);      // s_i, NX x N
+    static constexpr int nCond = oSv + NX * N - oR;
+    static_assert(LS * NV <= 3 * LD * NX, "the staged M tile fits the Z region");
+    static constexpr int nFront = oR - oU + (nExpm > nCond ? nExpm : nCond);
+    // solver view (after every thread holds its H_FF row part and g)
+    static constexpr int nSolver = WgLayout<NF>::doubles;
+    static constexpr int nDoubles = oU + (nFront > nSolver ? nFront : nSolver);
+    static constexpr size_t bytes =
+        sizeof(double) * nDoubles + sizeof(int) * (NF + NV) + ((MT + 15) & ~15);
+    static constexpr size_t lds_bytes = (bytes + 15) & ~(size_t)15;
+};
+
+template <int NX, int NU, int N>
+__device__ __forceinline__ void dense_mpc_one(const MpcArgs &a, int b, unsigned char *smem) {
+    using Lay = DenseLayout<NX, NU, N>;
+    constexpr int NS = Lay::NS, NV = Lay::NV, NF = Lay::NF, RW = Lay::RW, NH = NF / 2;
+    constexpr int LD = Lay::LD, LY = Lay::LY, LS = Lay::LS, NT = 2 * RW;
+    const WgIds T = wg_ids<RW>();
+    const int tid = T.tid, wv = T.wv, ln = T.ln, r = T.r, h = T.h;
+    double *D = reinterpret_cast<double *>(smem);
+    double *AB = D + Lay::oAB, *Ad = AB, *Bd = AB + NX * NX;
+    double *x0 = D + Lay::oX0, *xr = D + Lay::oXr, *fv = D + Lay::oF;
+
+    SolveProblem P;
+    P.nV = NV;
+    P.H = nullptr; P.f = nullptr; P.lb = nullptr; P.ub = nullptr;
+    P.gen_bounds = 1;
+    P.model = 2; P.nu = NU; P.N = N; P.nfeet = 2;  // input box u_min .. u_max (gen_bound)
+    P.fz_min = a.fz_min; P.fz_max = a.fz_max; P.fxy_max = a.fxy_max;
+    P.u_min = a.u_min; P.u_max = a.u_max;
+    P.contact = 0ull;
+    P.friction = 0;
+    P.mu = 0.0;
+    P.mA = 0; P.A = nullptr; P.a_colmajor = 0; P.lbA = nullptr; P.ubA = nullptr;
+    P.max_iter = a.max_iter;
+    GiCtx C;
+    C.wide = 1;
+    C.stamps = a.stamps;
+    C.cut = 0;
+    C.P = &P;
+    C.nfmax = NF;
+    C.L.ld = NF | 1;
+    C.L.R = nullptr; C.L.J = nullptr; C.L.g = nullptr;
+    C.L.xs = D + Lay::oXS;
+    C.L.xfull = D + Lay::oXF;
+    C.L.rowfix = D + Lay::oMisc;
+    C.L.ys = D + Lay::oMisc;
+    int *ip = reinterpret_cast<int *>(D + Lay::nDoubles);
+    C.L.fid = ip;
+    C.L.pos = ip + NF;
+    C.L.st = reinterpret_cast<unsigned char *>(ip + NF + NV);
+    C.L.cb = D + Lay::oCB;
+    MPCQP_STAMP_INIT(tst);
+
+    // ---- inputs: [Ac | Bc] Ts, x0, xref (coalesced over the workgroup)
+    {
+        const double *abg = a.lin + (size_t)b * NX * NS;
+        for (int e = tid; e < NX * NS; e += NT) D[Lay::oT + e] = abg[e] * a.Ts;
+        for (int e = tid; e < NX; e += NT) x0[e] = a.x0[(size_t)b * NX + e];
+        const double *xrg = a.xref + (size_t)b * NX * (N + 1);
+        for (int e = tid; e < NX * (N + 1); e += NT) xr[e] = xrg[e];
+    }
+    __syncthreads();
+    // ---- discretisation (wave 0) and the free map / bounds
+    if (wv == 0) {
+        wave_expm(NX, NS, D + Lay::oT, D + Lay::oWs, AB);
+        gi_setup(C);
+        if (C.nf > a.max_free) C.status = ST_BAD_DIMS;
+        if (ln == 0) {
+            D[Lay::oMisc] = (double)C.nf;
+            D[Lay::oMisc + 1] = (double)C.status;
+        }
+    }
+    __syncthreads();
+    MPCQP_STAMP(a.stamps, 11, tst);
+
+    // ---- Phi_a = Ad^a Bd, a = 0..N-1, by doubling: Phi[p .. p+nb) = Ad^p Phi[0 .. nb)
+    double *Phi = D + Lay::oPhi, *Pw0 = D + Lay::oPw, *Pw1 = Pw0 + LD * NX, *Pw2 = Pw1 + LD * NX;
+    for (int e = tid; e < NX * NU; e += NT) Phi[(e / NX) * LD + e % NX] = Bd[e];
+    __syncthreads();
+    {
+        const double *pw = Ad;
+        int ldp = NX;
+        double *nxt = Pw0, *oth = Pw1;
+        for (int p2 = 1; p2 < N; p2 *= 2) {
+            const int nb = p2 < N - p2 ? p2 : N - p2;
+            const bool more = 2 * p2 < N;
+            mfma_gemm<false>(NX, nb * NU, NX, pw, ldp, Phi, LD, Phi + p2 * NU * LD, LD, nullptr, 0,
+                             1.0, wv, 0, more ? 2 : 4);
+            if (more)
+                mfma_gemm<false>(NX, NX, NX, pw, ldp, pw, ldp, nxt, LD, nullptr, 0, 1.0, wv, 2, 2);
+            __syncthreads();
+            if (more) {
+                pw = nxt;
+                ldp = LD;
+                double *t_ = nxt;
+                nxt = oth;
+                oth = t_;
+            }
+        }
+    }
+    // ---- Z_{N-1} = P, Z_i = Q + Ad' Z_{i+1} Ad;  Y_i = Bd' Z_i into the stack's rows i NU ..
+    double *Y = D + Lay::oY;
+    for (int e = tid; e < NX * NX; e += NT) Pw0[(e / NX) * LD + e % NX] = a.pm[e];
+    __syncthreads();
+    {
+        double *Zc = Pw0, *Zn = Pw1;
+        for (int i = N - 1; i >= 0; --i) {
+            mfma_gemm<true>(NU, NX, NX, Bd, NX, Zc, LD, Y + i * NU, LY, nullptr, 0, 1.0, wv, 0, 2);
+            if (i > 0)
+                mfma_gemm<false>(NX, NX, NX, Zc, LD, Ad, NX, Pw2, LD, nullptr, 0, 1.0, wv, 2, 2);
+            __syncthreads();
+            if (i > 0) {
+                mfma_gemm<true>(NX, NX, NX, Ad, NX, Pw2, LD, Zn, LD, a.qm, NX, 1.0, wv, 0, 4);
+                __syncthreads();
+                double *t_ = Zc;
+                Zc = Zn;
+                Zn = t_;
+            }
+        }
+    }
+    MPCQP_STAMP(a.stamps, 1, tst);
+    // ---- gradient (wave 0): e_m = Ad^m x0 - xref_m, s_{N-1} = P e_N,
+    //      s_i = Q e_{i+1} + Ad' s_{i+1}, f_i = 2 Bd' s_i
+    if (wv == 0) {
+        double *xf = D + Lay::oXf, *sv = D + Lay::oSv;
+        if (ln < NX) xf[ln] = x0[ln];
+        wave_sync();
+        for (int m = 1; m <= N; ++m) {
+            if (ln < NX) {
+                double s = 0.0;
+#pragma unroll
+                for (int l = 0; l < NX; ++l) s += Ad[l * NX + ln] * xf[(m - 1) * NX + l];
+                xf[m * NX + ln] = s;
+            }
+            wave_sync();
+        }
+        for (int e = ln; e < NX * N; e += kWave) xf[NX + e] -= xr[NX + e];
+        wave_sync();
+        for (int i = N - 1; i >= 0; --i) {
+            if (ln < NX) {
+                const double *W = (i + 1 < N) ? a.qm : a.pm;
+                double s = 0.0;
+#pragma unroll
+                for (int l = 0; l < NX; ++l) s += W[l * NX + ln] * xf[(i + 1) * NX + l];
+                if (i + 1 < N) {
+#pragma unroll
+                    for (int l = 0; l < NX; ++l) s += Ad[ln * NX + l] * sv[(i + 1) * NX + l];
+                }
+                sv[i * NX + ln] = s;
+            }
+            wave_sync();
+        }
+        for (int e = ln; e < NV; e += kWave) {
+            const int i = e / NU, c = e % NU;
+            double s = 0.0;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) s += Bd[c * NX + l] * sv[i * NX + l];
+            fv[e] = 2.0 * s;
+        }
+    }
+    __syncthreads();
+    C.nf = (int)D[Lay::oMisc];
+    C.status = (int)D[Lay::oMisc + 1];
+    C.nfric = 0;
+    C.mt = 2 * C.nf;
+    C.c0 = 0.0;
+    const int nf = C.nf;
+    const bool ok = C.status == ST_OK && nf > 0;
+    MPCQP_STAMP(a.stamps, 4, tst);
+
+    // ---- H rows: 16-row tiles of M = Y Phi staged over the Z region; thread (r, h) takes
+    //      H(r, c) = 2 (M(r, (k_r - k_c) NU + c mod NU) + R(c_r, c_c) [k_r == k_c]), c = 2j + h
+    //      <= r (gi_run_wg's interleaved factorisation layout; identity beyond nf)
+    double hr[NH];
+#pragma unroll
+    for (int j = 0; j < NH; ++j) hr[j] = (r == 2 * j + h) ? 1.0 : 0.0;
+    double *stg = Pw0;
+    for (int r0 = 0; r0 < NV; r0 += 16) {
+        const int nrow = NV - r0 < 16 ? NV - r0 : 16;
+        const int ncol = ((r0 + nrow - 1) / NU + 1) * NU;  // columns a NU + c with a <= k_r
+        mfma_gemm<false>(nrow, ncol, NX, Y + r0, LY, Phi, LD, stg, LS, nullptr, 0, 1.0, wv, 0, 4);
+        __syncthreads();
+        if (ok && r >= r0 && r < r0 + nrow && r < nf) {
+            const int kr = r / NU, cr = r % NU;
+#pragma unroll
+            for (int j = 0; j < NH; ++j) {
+                const int c = 2 * j + h;
+                if (c <= r) {
+                    const int kc = c / NU, cc = c % NU;
+                    double v = stg[((kr - kc) * NU + cc) * LS + (r - r0)];
+                    if (kr == kc) v += a.rmat[cc * NU + cr];
+                    hr[j] = 2.0 * v;
+                }
+                if ((j & 7) == 7) step_fence();
+            }
+        }
+        __syncthreads();
+    }
+    const double g = (ok && r < nf) ? fv[C.L.fid[r]] : 0.0;
+    __syncthreads();  // the solver's workspace overlays the front
+    MPCQP_STAMP(a.stamps, 3, tst);
+    gi_run_wg<NF>(C, hr, g, D + Lay::oU);
+    MPCQP_STAMP_INIT(tw);
+    SolveOut O;
+    O.x = a.U + (size_t)b * NV;
+    O.cost = a.cost + b;
+    O.status = a.status + b;
+    O.iters = a.iters + b;
+    O.y = nullptr;
+    gi_write_wg<NF>(C, O);
+    MPCQP_STAMP(a.stamps, 9, tw);
+}
+
+}  // namespace mpcqp

@@ -1,0 +1,37 @@
+// fast_dense.hip -- the dense-model (whole-body, BASELINE config E) workgroup kernel,
+// dense_wg.hpp: one 4-wave workgroup per QP, FP64 MFMA condensing.
+#include <hip/hip_runtime.h>
+
+#include "../../include/mpcqp.h"
+#include "dense_wg.hpp"
+#include "fast_kernels.hpp"
+
+namespace mpcqp {
+namespace {
+
+template <int NX, int NU, int N>
+__global__ void __launch_bounds__(WgShape<NU * N>::THREADS, 2) k_dense_wg(MpcArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_d[];
+    for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+        dense_mpc_one<NX, NU, N>(a, b, smem_d);
+        __syncthreads();
+    }
+}
+
+template <int NX, int NU, int N>
+void add_dense(FastKernels &k) {
+    k.dense = (const void *)&k_dense_wg<NX, NU, N>;
+    k.dense_lds = DenseLayout<NX, NU, N>::lds_bytes;
+    k.dense_threads = WgShape<NU * N>::THREADS;
+    k.nx = NX;
+    k.nu = NU;
+}
+
+}  // namespace
+
+bool pick_fast_dense(int nx, int nu, int N, FastKernels &k) {
+    if (nx == 24 && nu == 6 && N == 16) { add_dense<24, 6, 16>(k); return true; }  // config E
+    return false;
+}
+
+}  // namespace mpcqp

@@ -26,6 +26,9 @@ struct FastKernels {
     const void *wg = nullptr;  // workgroup per QP for the overflow list (nf <= 6N)
     size_t wg_lds = 0;
     int wg_threads = 0;
+    const void *dense = nullptr;  // dense model (whole body): workgroup per QP, MFMA condensing
+    size_t dense_lds = 0;
+    int dense_threads = 0;
     const void *disc = nullptr, *cs = nullptr, *mpc = nullptr;
     size_t disc_lds = 0, cs_lds = 0, mpc_lds = 0;
     int nx = 0, nu = 0;
@@ -42,6 +45,8 @@ bool pick_fast_literal(int N, int nfmax, FastKernels &k);
 bool add_fast_pair(int model, int N, bool fric, int nfmax, FastKernels &k);
 // workgroup-per-QP kernels (fast_wg.hip) for the instances beyond the one-wave capacity
 bool add_fast_wg(int model, int N, bool fric, FastKernels &k);
+// dense-model kernels (fast_dense.hip): config E, 24/6/16
+bool pick_fast_dense(int nx, int nu, int N, FastKernels &k);
 
 #ifdef MPCQP_FAST_TU
 namespace {

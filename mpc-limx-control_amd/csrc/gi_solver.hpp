@@ -122,7 +122,7 @@ __device__ __forceinline__ double rowA(const SolveProblem &P, int r, int v) {
 // SRBM / literal bounds of variable v (gen_bounds mode)
 __device__ __forceinline__ void gen_bound(const SolveProblem &P, int v, double &lo, double &hi) {
     const int k = v / P.nu, c = v % P.nu;
-    if (P.model == 1) { lo = P.u_min; hi = P.u_max; return; }
+    if (P.model != 0) { lo = P.u_min; hi = P.u_max; return; }  // literal / dense: input box
     const int s = c / 3, comp = c % 3;
     if ((P.contact >> (2 * k + s)) & 1ull) {
         if (comp == 2) { lo = P.fz_min; hi = P.fz_max; }

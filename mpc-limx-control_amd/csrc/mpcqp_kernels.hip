@@ -70,11 +70,16 @@ __global__ void __launch_bounds__(64) k_condense(CondenseArgs a) {
     } else {
         double *T = ws;
         double lin[8];
-        if (a.lin)
+        if (a.lin && mc.model != 2)
 #pragma unroll
             for (int i = 0; i < 8; ++i) lin[i] = a.lin[(size_t)b * 8 + i];
-        wave_build_model(mc, lin, a.Ac ? a.Ac + (size_t)b * nx * nx : nullptr,
-                         a.Bc ? a.Bc + (size_t)b * nx * mc.nu : nullptr, T);
+        const double *Acb = a.Ac ? a.Ac + (size_t)b * nx * nx : nullptr;
+        const double *Bcb = a.Bc ? a.Bc + (size_t)b * nx * mc.nu : nullptr;
+        if (mc.model == 2) {  // dense model: lin = [Ac | Bc] per instance
+            Acb = a.lin + (size_t)b * nx * ns;
+            Bcb = Acb + nx * nx;
+        }
+        wave_build_model(mc, lin, Acb, Bcb, T);
         wave_expm(nx, ns, T, ws + nx * ns, AB);
     }
     if (a.ABout)
@@ -765,7 +770,10 @@ int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
     if (rc) return rc;
     if (m->model == MPCQP_MODEL_SRBM && (m->nx != 13 || m->nu != 6)) return MPCQP_ERR_BAD_DIMS;
     if (m->model == MPCQP_MODEL_LITERAL && (m->nx != 13 || m->nu != 3)) return MPCQP_ERR_BAD_DIMS;
-    if (m->model != MPCQP_MODEL_SRBM && m->model != MPCQP_MODEL_LITERAL) return MPCQP_ERR_BAD_ARG;
+    if (m->model != MPCQP_MODEL_SRBM && m->model != MPCQP_MODEL_LITERAL &&
+        m->model != MPCQP_MODEL_DENSE)
+        return MPCQP_ERR_BAD_ARG;
+    if (m->model == MPCQP_MODEL_DENSE && !(m->u_min < m->u_max)) return MPCQP_ERR_BAD_ARG;
     if (m->constraints != MPCQP_CONS_BOX && m->constraints != MPCQP_CONS_FRICTION)
         return MPCQP_ERR_BAD_ARG;
     const int nfmax = m->max_free > 0 ? m->max_free : m->nu * m->N;
@@ -802,8 +810,12 @@ int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
     const bool fric = m->model == MPCQP_MODEL_SRBM && m->constraints == MPCQP_CONS_FRICTION;
     const bool bounds_ok = m->model == MPCQP_MODEL_LITERAL ||
                            (m->fz_min < m->fz_max && m->fxy_max > 0.0);
-    c->fast = is_diag(m->Q, nx) && is_diag(m->P, nx) && bounds_ok && nu <= 6 &&
-              pick_fast(m->model, nx, nu, m->N, fric, nfmax, c->fk);
+    c->fast = m->model != MPCQP_MODEL_DENSE && is_diag(m->Q, nx) && is_diag(m->P, nx) &&
+              bounds_ok && nu <= 6 && pick_fast(m->model, nx, nu, m->N, fric, nfmax, c->fk);
+    if (m->model == MPCQP_MODEL_DENSE && nfmax <= 128 && pick_fast_dense(nx, nu, m->N, c->fk)) {
+        c->fast = true;  // dense Q/R/P allowed: the kernel reads them whole
+        set_lds(c->fk.dense, c->fk.dense_lds);
+    }
     if (!c->fast && nfmax > kWave) {  // the generic one-wave solver holds 64 free variables
         mpcqp_ctx_destroy(c);
         return MPCQP_ERR_BAD_DIMS;
@@ -825,6 +837,7 @@ int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
 
 int mpcqp_ctx_fast_path(const mpcqp_ctx *c) {
     if (!c || !c->fast) return 0;
+    if (c->fk.dense) return 3;
     return c->fk.pair ? 2 : 1;
 }
 
@@ -961,6 +974,8 @@ static MpcArgs mpc_args(mpcqp_ctx *c, int B) {
     for (int i = 0; i < 9; ++i) a.Ibinv[i] = c->Ibinv[i];
     a.qd = c->dqd;
     a.pd = c->dpd;
+    a.qm = c->dQ;
+    a.pm = c->dP;
     a.rmat = c->dR;
     a.fz_min = m.fz_min;
     a.fz_max = m.fz_max;
@@ -1095,7 +1110,7 @@ int mpcqp_batch_discretize(mpcqp_ctx *c, int B, const double *lin, double *AB) {
     hipSetDevice(c->device);
     int rc;
     tbegin(c, 0);
-    if (c->fast) {
+    if (c->fast && c->fk.disc) {
         FastArgs a = fast_args(c, B);
         a.lin = lin;
         a.AB = AB;
@@ -1135,7 +1150,7 @@ int mpcqp_batch_condense_solve(mpcqp_ctx *c, int B, const double *AB, const doub
     if (c->m.model == MPCQP_MODEL_SRBM && !contact) return MPCQP_ERR_BAD_ARG;
     if (B == 0) return MPCQP_OK;
     hipSetDevice(c->device);
-    if (c->fast) {
+    if (c->fast && c->fk.cs) {
         FastArgs a = fast_args(c, B);
         a.AB = const_cast<double *>(AB);
         a.x0 = x0;
@@ -1182,7 +1197,14 @@ int mpcqp_batch_solve(mpcqp_ctx *c, int B, const double *x0, const double *xref,
         a.status = status;
         a.iters = iters;
         tbegin(c, 1);
-        const int rc = launch_mpc(c, false, B, &a);
+        int rc;
+        if (c->fk.dense) {  // one workgroup per QP
+            void *args[] = {&a};
+            rc = hip_status(hipLaunchKernel(c->fk.dense, dim3(B), dim3(c->fk.dense_threads), args,
+                                            c->fk.dense_lds, c->stream));
+        } else {
+            rc = launch_mpc(c, false, B, &a);
+        }
         tend(c, 1);
         return rc;
     }
@@ -1208,7 +1230,8 @@ int mpcqp_batch_solve_host(mpcqp_ctx *c, int B, const double *x0, const double *
     if (B == 0) return MPCQP_OK;
     hipSetDevice(c->device);
     const size_t nx = c->m.nx, N = c->m.N, nV = (size_t)c->m.nu * c->m.N;
-    const size_t n_x0 = nx * B, n_xr = nx * (N + 1) * B, n_lin = 8 * (size_t)B, n_u = nV * B;
+    const size_t lin_w = c->m.model == MPCQP_MODEL_DENSE ? nx * (nx + c->m.nu) : 8;
+    const size_t n_x0 = nx * B, n_xr = nx * (N + 1) * B, n_lin = lin_w * B, n_u = nV * B;
     const size_t bytes = sizeof(double) * (n_x0 + n_xr + n_lin + n_u + B) +
                          sizeof(uint64_t) * B + 2 * sizeof(int) * B + 64;
     if (c->hbuf_cap < bytes) {

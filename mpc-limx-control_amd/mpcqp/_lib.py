@@ -16,7 +16,7 @@ MPCQP_OK = 0
 STATUS = {0: "OK", 1: "BAD_DIMS", 2: "INFEASIBLE", 3: "ITER_LIMIT", 4: "NOT_PD", 5: "DEVICE",
           6: "BAD_ARG", 7: "NO_DEVICE"}
 MPCQP_INFTY = 1e20
-MODEL_SRBM, MODEL_LITERAL = 0, 1
+MODEL_SRBM, MODEL_LITERAL, MODEL_DENSE = 0, 1, 2
 CONS_BOX, CONS_FRICTION = 0, 1
 A_ROWMAJOR, A_COLMAJOR = 0, 1
 

@@ -54,7 +54,7 @@ class BatchEngine:
         dev = f"cuda:{self.device}"
         out = {k: t.from_numpy(np.ascontiguousarray(batch[k])).to(dev)
                for k in ("x0", "xref", "lin")}
-        out["contact"] = t.from_numpy(batch["contact"].view(np.int64)).to(dev)
+        out["contact"] = t.from_numpy(np.ascontiguousarray(batch["contact"]).view(np.int64)).to(dev)
         B = batch["x0"].shape[0]
         out["U"] = t.zeros((B, self.nV), dtype=t.float64, device=dev)
         out["cost"] = t.zeros(B, dtype=t.float64, device=dev)
@@ -88,8 +88,8 @@ class BatchEngine:
     def fused_kernel(self) -> str:
         """name of the kernel mpcqp_batch_solve launches: k_mpc_pair (two QPs per wave),
         k_mpc (one QP per wave) or the generic k_condense + k_solve pair"""
-        return {2: "k_mpc_pair", 1: "k_mpc"}.get(lib().mpcqp_ctx_fast_path(self.ctx),
-                                                  "k_condense+k_solve")
+        return {3: "k_dense_wg", 2: "k_mpc_pair", 1: "k_mpc"}.get(
+            lib().mpcqp_ctx_fast_path(self.ctx), "k_condense+k_solve")
 
     def discretize(self, d, AB=None):
         """stage 1: linearise + exp(M Ts) -> [Ad | Bd] per instance"""

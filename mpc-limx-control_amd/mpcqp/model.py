@@ -18,7 +18,7 @@ import ctypes as C
 
 import numpy as np
 
-from ._lib import CONS_BOX, CONS_FRICTION, MODEL_LITERAL, MODEL_SRBM, Model
+from ._lib import CONS_BOX, CONS_FRICTION, MODEL_DENSE, MODEL_LITERAL, MODEL_SRBM, Model
 
 MASS = 9.585
 INERTIA = np.array([[140110.479e-06, 534.939e-06, 28184.116e-06],
@@ -49,14 +49,34 @@ def static_foot_offsets():
     return left, right
 
 
+# Config E (BASELINE configs[4]): the whole-body linearisation of TRON1 -- 24 states (6 base + 6
+# joint positions, 12 velocities), 6 joint torques, N = 16.  The reference computes its
+# whole-body kinematics with Pinocchio (include/pinocchio_kinematics.h) and has no whole-body
+# MPC, so the weights, torque limit and sample time are build-chosen; the
+# per-instance continuous model [Ac | Bc] comes from workload.whole_body_models.
+TS_E = 0.01
+TAU_MAX_E = 5.0  # about ten active torque bounds per QP at the optimum
+Q_DIAG_E = np.array([200.0] * 6 + [50.0] * 6 + [2.0] * 6 + [1.0] * 6)
+R_E = 1e-3
+
+
 def model_params(config: str = "B", N: int | None = None) -> dict:
     """Host description of one benchmark configuration.
 
     A0  reference qp_test plant (4/2/15) -- single-instance API only, see qp_harness()
     A   13/6/10 SRBM, box, one QP          B  13/6/10 SRBM, box (the metric model)
     C   13/6/20 SRBM, box + friction       L  13/3/20 reference-literal mpcQP model
+    E   24/6/16 whole-body dense model, torque box (one workgroup per QP, MFMA condensing)
     """
     fzmax = 4.0 * MASS * GRAVITY
+    if config == "E":
+        Nh = 16 if N is None else N
+        Q = np.diag(Q_DIAG_E)
+        return dict(config="E", nx=24, nu=6, N=Nh, model=MODEL_DENSE, friction=CONS_BOX,
+                    constraints=CONS_BOX, Ts=TS_E, mass=MASS, mu=MU, Ib=INERTIA.copy(),
+                    fz_min=0.0, fz_max=fzmax, fxy_max=MU * fzmax, u_min=-TAU_MAX_E,
+                    u_max=TAU_MAX_E, Q=Q, R=R_E * np.eye(6), P=10.0 * Q, max_iter=0,
+                    max_free=0)
     if config in ("A", "B", "C", "D"):
         nu, model = 6, MODEL_SRBM
         Nh = 20 if config == "C" else 10

@@ -14,7 +14,7 @@ import math
 
 import numpy as np
 
-from .model import GRAVITY, STANCE_TIME, SWING_TIME, static_foot_offsets
+from .model import GRAVITY, INERTIA, MASS, STANCE_TIME, SWING_TIME, static_foot_offsets
 
 DEFAULT_SEED = 20250404
 
@@ -78,10 +78,61 @@ def contact_masks(gait: str, N: int, Ts: float, phase) -> np.ndarray:
     return out
 
 
+def whole_body_models(S: int, rng) -> np.ndarray:
+    """S linearised whole-body models of a TRON1-like robot, [Ac | Bc] (24 x 30, column-major
+    flattened): q = (base xyz, base rpy, 6 joints), v = dq, and
+        dv = M^-1 (Sel tau - K dq - D v)
+    with a random SPD mass matrix around the reference's body mass / inertia
+    (include/mpcQP.h:18-22) and light legs, a contact / gravity stiffness K and damping D
+    (build-chosen: the reference's whole-body path is Pinocchio FK only), torques on the six
+    joints."""
+    n = 12
+    Md = np.concatenate([np.full(3, MASS), np.diag(INERTIA), np.full(6, 0.05)])
+    A = rng.normal(0.0, 0.3, (S, n, n))
+    M = 0.02 * A @ A.transpose(0, 2, 1) + np.diag(Md)[None]
+    Kd = np.concatenate([np.full(3, 2000.0), np.full(3, 200.0), np.full(6, 20.0)])
+    Kr = rng.normal(0.0, 1.0, (S, n, n))
+    K = np.diag(Kd)[None] + (Kr + Kr.transpose(0, 2, 1))
+    Dd = np.concatenate([np.full(3, 40.0), np.full(3, 4.0), np.full(6, 0.5)])
+    D = np.diag(Dd)[None] + 0.1 * np.abs(rng.normal(0.0, 1.0, (S, 1, 1))) * np.eye(n)[None]
+    Minv = np.linalg.inv(M)
+    Ac = np.zeros((S, 24, 24))
+    Ac[:, :n, n:] = np.eye(n)
+    Ac[:, n:, :n] = -Minv @ K
+    Ac[:, n:, n:] = -Minv @ D
+    Bc = np.zeros((S, 24, 6))
+    Bc[:, n:, :] = Minv[:, :, 6:]  # Sel = [0; I6]: the joint torques
+    AB = np.concatenate([Ac, Bc], axis=2)  # [Ac | Bc], 24 x 30
+    return np.ascontiguousarray(AB.transpose(0, 2, 1).reshape(S, -1))  # column-major per model
+
+
+def make_dense_batch(p: dict, B: int, seed: int = DEFAULT_SEED, candidates: int = 16):
+    """config E: S states x C candidates; per state a linearised whole-body model and a
+    deviation x0 (base pose +-0.02, joints +-0.3 rad, velocities +-1), per candidate a joint
+    target held over the horizon (xref, N(0, 0.1) rad)"""
+    rng = np.random.default_rng(seed)
+    nx, N = p["nx"], p["N"]
+    C = max(1, min(candidates, B))
+    S = (B + C - 1) // C
+    AB = whole_body_models(S, rng)
+    x0 = np.concatenate([rng.uniform(-0.02, 0.02, (S, 6)), rng.uniform(-0.3, 0.3, (S, 6)),
+                         rng.uniform(-1.0, 1.0, (S, 12))], axis=1)
+    tgt = rng.normal(0.0, 0.1, (S, C, 6))
+    xref = np.zeros((S, C, N + 1, nx))
+    xref[:, :, :, 6:12] = tgt[:, :, None, :]
+    rep = lambda a: np.repeat(a, C, axis=0)[:B]
+    return dict(x0=np.ascontiguousarray(rep(x0)),
+                xref=np.ascontiguousarray(xref.reshape(S * C, N + 1, nx)[:B]),
+                lin=np.ascontiguousarray(rep(AB)), contact=np.zeros(B, dtype=np.uint64))
+
+
 def make_batch(p: dict, B: int, seed: int = DEFAULT_SEED, candidates: int = 16,
                gait: str = "alternating"):
     """-> dict(x0 [B,13], xref [B,N+1,13], lin [B,8], contact [B] uint64).  `gait` picks the
-    contact schedules of the candidates (GAITS); the default is the reference's calculateGait."""
+    contact schedules of the candidates (GAITS); the default is the reference's calculateGait.
+    The dense model (config E) takes make_dense_batch."""
+    if p.get("model") == 2:
+        return make_dense_batch(p, B, seed, candidates)
     rng = np.random.default_rng(seed)
     N, nx, Ts = p["N"], p["nx"], p["Ts"]
     C = max(1, min(candidates, B))

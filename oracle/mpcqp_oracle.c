@@ -914,6 +914,51 @@ int orc_srbm_batch(const orc_srbm_cfg *cfg, int B, const double *x0, const doubl
     return ORC_OK;
 }
 
+/* dense model, one instance (config E) -- see mpcqp_oracle.h */
+static int dense_one(const orc_dense_cfg *cfg, const double *x0, const double *xref,
+                     const double *AB, double *U, double *cost, int *iters, double *Hout,
+                     double *fout) {
+    const int nx = cfg->nx, nu = cfg->nu, N = cfg->N, nV = nu * N;
+    double *Ad = malloc(sizeof(double) * nx * (nx + nu)), *Bd = Ad + nx * nx;
+    orc_discretize(nx, nu, cfg->Ts, AB, AB + nx * nx, Ad, Bd);
+    double *H = Hout ? Hout : malloc(sizeof(double) * nV * nV);
+    double *f = fout ? fout : malloc(sizeof(double) * nV);
+    double *lb = malloc(sizeof(double) * nV * 2), *ub = lb + nV;
+    orc_build_qp(nx, nu, N, Ad, Bd, cfg->Q, cfg->R, cfg->P, NULL, NULL, 0, 0, x0, xref, H, f,
+                 NULL, NULL, NULL, NULL, NULL, NULL, NULL);
+    for (int v = 0; v < nV; ++v) { lb[v] = cfg->u_min; ub[v] = cfg->u_max; }
+    int st = orc_solve_qp(nV, H, f, 0, NULL, 0, lb, ub, NULL, NULL, NULL, cfg->max_iter, U,
+                          cost, iters, NULL, NULL);
+    if (!Hout) free(H);
+    if (!fout) free(f);
+    free(lb);
+    free(Ad);
+    return st;
+}
+
+int orc_dense_batch(const orc_dense_cfg *cfg, int B, const double *x0, const double *xref,
+                    const double *AB, double *U, double *cost, int *status, int *iters,
+                    double *H_out, double *f_out, int nthreads) {
+    const int nx = cfg->nx, nV = cfg->nu * cfg->N, ab = cfg->nx * (cfg->nx + cfg->nu);
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+    for (int b = 0; b < B; ++b) {
+        int it = 0;
+        double c = 0.0;
+        const int st = dense_one(cfg, x0 + (size_t)b * nx, xref + (size_t)b * nx * (cfg->N + 1),
+                                 AB + (size_t)b * ab, U + (size_t)b * nV, &c, &it,
+                                 H_out ? H_out + (size_t)b * nV * nV : NULL,
+                                 f_out ? f_out + (size_t)b * nV : NULL);
+        if (cost) cost[b] = c;
+        if (status) status[b] = st;
+        if (iters) iters[b] = it;
+    }
+    (void)nthreads;
+    return ORC_OK;
+}
+
 int orc_srbm_plant(const orc_srbm_cfg *cfg, const double *lin, double *x, const double *u) {
     double Ac[13 * 13], Bc[13 * 6], Ad[13 * 13], Bd[13 * 6];
     orc_model_srbm(lin, cfg->mass, cfg->Ib, Ac, Bc);

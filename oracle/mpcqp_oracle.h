@@ -124,6 +124,26 @@ void orc_srbm_bounds(const orc_srbm_cfg *cfg, uint64_t contact, double *lb, doub
  * Pade expm restated).  Returns the discretisation status. */
 int orc_srbm_plant(const orc_srbm_cfg *cfg, const double *lin, double *x, const double *u);
 
+/* ---- dense model (BASELINE config E: the whole-body linearisation, 24 states) ------------
+ * Per instance the continuous model [Ac | Bc] (nx x (nx+nu), column-major) is given, as the
+ * upstream whole-body linearisation hands it over; the step is the reference's own path:
+ * QPSolver::discretizeSystem (src/QPSolver.cpp:21-29, Eigen expm) -> buildQPParams
+ * (:31-81, literal dense B'QB with full Q/R/P) -> the corrected QP with the input box
+ * u_min <= u <= u_max (:67-68) -> Goldfarb-Idnani.  x0 [B][nx], xref [B][N+1][nx],
+ * AB [B][nx*(nx+nu)], U [B][nu*N]. */
+typedef struct {
+    int nx, nu, N;
+    double Ts;
+    const double *Q, *R, *P; /* nx*nx, nu*nu, nx*nx column-major (dense) */
+    double u_min, u_max;
+    int max_iter;
+} orc_dense_cfg;
+
+int orc_dense_batch(const orc_dense_cfg *cfg, int B, const double *x0, const double *xref,
+                    const double *AB, double *U, double *cost, int *status, int *iters,
+                    double *H_out /* nullable [B][nV][nV] */, double *f_out /* nullable */,
+                    int nthreads);
+
 /* ---- state estimator and leg kinematics ------------------------ */
 /* stateEstimator::update (include/stateEstimator.h:217-337), one robot: xhat[12], P[144]
  * (col-major) updated in place from eePos[6], eeVel[6] (feet relative to the base, world

@@ -43,6 +43,12 @@ def build() -> str:
     return _LIB_PATH
 
 
+class DenseCfg(C.Structure):
+    _fields_ = [("nx", C.c_int), ("nu", C.c_int), ("N", C.c_int), ("Ts", C.c_double),
+                ("Q", C.c_void_p), ("R", C.c_void_p), ("P", C.c_void_p), ("u_min", C.c_double),
+                ("u_max", C.c_double), ("max_iter", C.c_int)]
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -64,6 +70,8 @@ def lib():
         L.orc_gait_contact_mask.restype = C.c_uint64
         L.orc_srbm_batch.argtypes = [C.POINTER(SrbmCfg), C.c_int, _dp, _dp, _dp, _up, _dp, _dp,
                                      _ip, _ip, C.c_void_p, C.c_void_p, C.c_int]
+        L.orc_dense_batch.argtypes = [C.POINTER(DenseCfg), C.c_int, _dp, _dp, _dp, _dp, _dp, _ip,
+                                      _ip, C.c_void_p, C.c_void_p, C.c_int]
         L.orc_srbm_bounds.argtypes = [C.POINTER(SrbmCfg), C.c_uint64, _dp, _dp]
         L.orc_srbm_plant.argtypes = [C.POINTER(SrbmCfg), _dp, _dp, _dp]
         L.orc_fk_feet.argtypes = [_dp, _dp, _dp]
@@ -254,4 +262,30 @@ def fk_feet(q, rpy):
     out = np.zeros(6)
     lib().orc_fk_feet(np.ascontiguousarray(q, dtype=np.float64),
                       np.ascontiguousarray(rpy, dtype=np.float64), out)
+    return out
+
+
+def dense_batch(p, x0, xref, AB, nthreads=0, want_hf=False):
+    """config E (dense continuous model per instance): discretize -> literal dense condensing ->
+    box-constrained Goldfarb-Idnani.  AB [B, nx*(nx+nu)] = [Ac | Bc] column-major."""
+    keep = [_f(p["Q"]), _f(p["R"]), _f(p["P"])]
+    cfg = DenseCfg(p["nx"], p["nu"], p["N"], p["Ts"], keep[0].ctypes.data, keep[1].ctypes.data,
+                   keep[2].ctypes.data, p["u_min"], p["u_max"], p.get("max_iter", 0))
+    B = int(x0.shape[0])
+    nV = p["nu"] * p["N"]
+    U = np.zeros(B * nV)
+    cost = np.zeros(B)
+    status = np.zeros(B, np.int32)
+    iters = np.zeros(B, np.int32)
+    H = np.zeros(B * nV * nV) if want_hf else None
+    f = np.zeros(B * nV) if want_hf else None
+    lib().orc_dense_batch(C.byref(cfg), B, np.ascontiguousarray(x0, dtype=np.float64).reshape(-1),
+                          np.ascontiguousarray(xref, dtype=np.float64).reshape(-1),
+                          np.ascontiguousarray(AB, dtype=np.float64).reshape(-1), U, cost, status,
+                          iters, _ptr(H), _ptr(f), int(nthreads))
+    del keep
+    out = dict(U=U.reshape(B, nV), cost=cost, status=status, iters=iters)
+    if want_hf:
+        out["H"] = H.reshape(B, nV, nV).transpose(0, 2, 1)
+        out["f"] = f.reshape(B, nV)
     return out

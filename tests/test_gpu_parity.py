@@ -566,3 +566,77 @@ def test_overflow_full_size_mixed_gait(gpu, orc):
     ref = orc.srbm_batch(p, sub["x0"], sub["xref"], sub["lin"], sub["contact"])
     for j, i in enumerate(idx):
         assert u_close(U1[i], ref["U"][j]), i
+
+
+# ------------------------------------------------------------- config E: the dense model
+def test_dense_condense_vs_oracle(gpu, orc):
+    """config E (24/6/16 whole-body model, dense Q/R/P): the generic condensing kernel
+    (k_condense: Pade expm + Phi chain, full H to HBM) against the oracle's literal dense
+    B'QB (src/QPSolver.cpp:31-81) at <= 1e-12"""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("E")
+    batch = mpcqp.make_batch(p, 48, seed=5)
+    eng = BatchEngine(p)
+    d = eng.upload(batch)
+    H, f = eng.condense(d)
+    eng.sync()
+    Hg = H.cpu().numpy().transpose(0, 2, 1)
+    fg = f.cpu().numpy()
+    eng.close()
+    ref = orc.dense_batch(p, batch["x0"], batch["xref"], batch["lin"], want_hf=True)
+    for i in range(48):
+        assert rel_err(Hg[i], ref["H"][i]) <= TOL_COND, i
+        assert rel_err(fg[i], ref["f"][i]) <= TOL_COND, i
+
+
+def test_dense_fused_vs_oracle(gpu, orc):
+    """config E through the fused workgroup kernel (k_dense_wg: expm, MFMA condensing, 96-free-
+    variable Goldfarb-Idnani): every instance solved and written once, U / cost / iterations
+    against the oracle"""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("E")
+    B = 256
+    batch = mpcqp.make_batch(p, B, seed=9)
+    eng = BatchEngine(p)
+    assert eng.fused_kernel == "k_dense_wg"
+    d = _prefilled(eng, batch)
+    eng.solve(d)
+    eng.sync()
+    o = {k: d[k].cpu().numpy() for k in ("U", "cost", "status", "iters")}
+    eng.close()
+    ref = orc.dense_batch(p, batch["x0"], batch["xref"], batch["lin"])
+    assert np.all(ref["status"] == 0)
+    np.testing.assert_array_equal(o["status"], ref["status"])
+    assert ref["iters"].mean() > 3  # torque bounds bind
+    bad = [i for i in range(B) if not u_close(o["U"][i], ref["U"][i])]
+    assert not bad, bad[:10]
+    np.testing.assert_allclose(o["cost"], ref["cost"], rtol=1e-9, atol=1e-9)
+    assert np.mean(o["iters"] == ref["iters"]) >= 0.95
+
+
+def test_dense_full_size_properties(gpu, orc):
+    """config E at its BASELINE batch (16,384): all solved, deterministic, sample vs oracle"""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("E")
+    B = 16384
+    batch = mpcqp.make_batch(p, B, seed=13)
+    eng = BatchEngine(p)
+    d = _prefilled(eng, batch)
+    eng.solve(d)
+    eng.sync()
+    U1 = d["U"].cpu().numpy().copy()
+    st = d["status"].cpu().numpy().copy()
+    eng.solve(d)
+    eng.sync()
+    U2 = d["U"].cpu().numpy()
+    eng.close()
+    assert np.all(st == 0)
+    np.testing.assert_array_equal(U1, U2)
+    idx = np.random.default_rng(2).choice(B, 96, replace=False)
+    sub = {k: batch[k][idx] for k in batch}
+    ref = orc.dense_batch(p, sub["x0"], sub["xref"], sub["lin"])
+    for j, i in enumerate(idx):
+        assert u_close(U1[i], ref["U"][j]), i
