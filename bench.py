@@ -503,7 +503,10 @@ def main():
             roof["executed_tflops"] = per_launch / (mpc_ms * 1e-3) / 1e12
             roof["pipe_frac"] = roof["executed_tflops"] / FP64_PEAK_TFLOPS
             roof["executed_source"] = f"profiles/{ex.get('file', 'pmc_flops.json')} " \
-                                      "(SQ_INSTS_VALU_{FMA,MUL,ADD}_F64 x 64 lanes)"
+                                      "(64 lanes x SQ_INSTS_VALU_FLOPS_FP64, a per-wave-" \
+                                      "instruction count: EXEC-masked lanes included, an " \
+                                      "upper bound; + MFMA ops)"
+            roof["executed_tag"] = ex.get("tag")
         out["roofline"] = roof
         if weak:
             cfg["weak"] = weak

@@ -75,7 +75,8 @@ __global__ void __launch_bounds__(64) k_condense(CondenseArgs a) {
             for (int i = 0; i < 8; ++i) lin[i] = a.lin[(size_t)b * 8 + i];
         const double *Acb = a.Ac ? a.Ac + (size_t)b * nx * nx : nullptr;
         const double *Bcb = a.Bc ? a.Bc + (size_t)b * nx * mc.nu : nullptr;
-        if (mc.model == 2) {  // dense model: lin = [Ac | Bc] per instance
+        if (mc.model == 2 && a.lin) {  // dense model: lin = [Ac | Bc] per instance
+            // (the single-instance entry points pass model 2 with Ac/Bc and no lin)
             Acb = a.lin + (size_t)b * nx * ns;
             Bcb = Acb + nx * nx;
         }

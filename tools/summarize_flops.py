@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
 """Summarize a tools/pmc_flops.sh output directory into profiles/pmc_flops.json: executed FP64
 work of one kernel per launch (median over its dispatches).
-  executed_flops_per_launch  SQ_INSTS_VALU_FLOPS_FP64 (per-lane FLOPs of every FP64 VALU
-                             instruction, MFMA excluded) + 512 x SQ_INSTS_VALU_MFMA_MOPS_F64
-  lane_flops_upper_bound     64 x (2 FMA + MUL + ADD) F64 instructions (every lane counted)
+  executed_flops_per_launch  64 lanes x SQ_INSTS_VALU_FLOPS_FP64 + 512 x SQ_INSTS_VALU_MFMA_MOPS_F64.
+                             SQ_INSTS_VALU_FLOPS_FP64 counts per WAVE instruction (it equals
+                             2 FMA + MUL + ADD + TRANS F64 instructions exactly, profiles/
+                             pmc_flops.json r02_v1), so x 64 counts every lane, EXEC-masked
+                             lanes included: an upper bound of the lane FLOPs executed
+  lane_flops_upper_bound     the same bound from the per-type counters
   mfma_busy_frac             SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs)
 Usage: tools/summarize_flops.py PROFDIR TAG --kernel k_mpc_pair [--config B --batch 65536]"""
 import argparse
@@ -42,9 +45,10 @@ def main():
     except OSError:
         gr = {}
     g = lambda k: sq.get(k, 0.0)
-    executed = g("SQ_INSTS_VALU_FLOPS_FP64") + 512.0 * g("SQ_INSTS_VALU_MFMA_MOPS_F64")
+    executed = 64.0 * g("SQ_INSTS_VALU_FLOPS_FP64") + 512.0 * g("SQ_INSTS_VALU_MFMA_MOPS_F64")
     upper = 64.0 * (2 * g("SQ_INSTS_VALU_FMA_F64") + g("SQ_INSTS_VALU_MUL_F64") +
-                    g("SQ_INSTS_VALU_ADD_F64"))
+                    g("SQ_INSTS_VALU_ADD_F64") + g("SQ_INSTS_VALU_TRANS_F64")) + \
+        512.0 * g("SQ_INSTS_VALU_MFMA_MOPS_F64")
     out = dict(tag=a.tag, kernel=a.kernel, config=a.config, batch=a.batch, file=a.out,
                counters=sq, dispatches=n, grbm=gr,
                executed_flops_per_launch=executed, lane_flops_upper_bound=upper,
