@@ -521,7 +521,8 @@ def main():
                                          ("C@65536", "C", 65536, None),
                                          ("L@65536", "L", 65536, None),
                                          ("B-standing@65536", "B", 65536, "standing"),
-                                         ("C-mixed@65536", "C", 65536, "mixed")):
+                                         ("C-mixed@65536", "C", 65536, "mixed"),
+                                         ("E@16384", "E", 16384, None)):
                 try:
                     per[name] = time_config(conf, Bc, args.seed, gait=gait)
                 except Exception as exc:  # report, never hide

@@ -44,6 +44,9 @@
  * mpcqp_rollout                   the closed loop of src/qpSolver_test.cpp:38-90, batched
  * mpcqp_fk_feet                   PinocchioKinematics::forwardKinematics + getLinkPosition
  *                                 (include/pinocchio_kinematics.h:30-43), batched
+ * mpcqp_ctx_fk_feet_host          the same, host pointers (mpcQP::buildSystemModel's FK,
+ *                                 include/mpcQP.h:125-137)
+ * mpcqp_ctx_reserve               (new) pre-sizes the context's buffers (no allocation per tick)
  * mpcqp_kf_update                 stateEstimator::update (include/stateEstimator.h:217-337),
  *                                 batched
  */
@@ -158,6 +161,11 @@ int mpcqp_ctx_destroy(mpcqp_ctx *ctx);
  * stream; mpcqp_sync waits for it. */
 int mpcqp_set_stream(mpcqp_ctx *ctx, void *stream);
 int mpcqp_sync(mpcqp_ctx *ctx);
+/* Size every context-owned scratch buffer (host staging, overflow list, rollout buffers, the
+ * generic path's [Ad|Bd] and H/f) for batches of up to B instances, so that no call on the
+ * solve path allocates device memory afterwards (SURVEY.md 8b ownership: "no allocation on
+ * the solve path after create").  Larger batches still work; they grow the buffers once. */
+int mpcqp_ctx_reserve(mpcqp_ctx *ctx, int B);
 
 /* 0 when the context runs the generic kernels; 1 when it runs the compile-time-dimension
  * fused kernel, one QP per wavefront (13/6/{10,20} SRBM, 13/3/{10,20} literal, diagonal Q and
@@ -243,6 +251,10 @@ int mpcqp_rollout(mpcqp_ctx *ctx, int S, int C, int K, double *state, double *fe
  * (include/MPCParam.h:13-38), at q = 0 equal to static_foot_offset_* (:64-72). */
 int mpcqp_fk_feet(void *stream, int R, const double *q, const double *rpy, int rpy_stride,
                   double *feet);
+/* Host-pointer form for controllers (MPC::computeSupportFootForce, one robot per tick): stages
+ * q/rpy through the context's buffer, runs k_fk_feet on the context's stream, synchronous. */
+int mpcqp_ctx_fk_feet_host(mpcqp_ctx *ctx, int R, const double *q, const double *rpy,
+                           int rpy_stride, double *feet);
 /* One step of stateEstimator::update (include/stateEstimator.h:217-337) for R robots:
  * xhat [R][12] (p, v, foot positions), P [R][144] (column-major) updated in place from
  * eePos/eeVel [R][6] (feet relative to the base), contact [R][2], quat [R][4] (x y z w),

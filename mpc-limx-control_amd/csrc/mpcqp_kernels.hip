@@ -534,6 +534,8 @@ struct mpcqp_ctx {
     // closed-loop rollout workspace
     void *rbuf = nullptr;
     size_t rbuf_cap = 0;
+    void *fkbuf = nullptr;  // mpcqp_ctx_fk_feet_host staging
+    size_t fkbuf_cap = 0;
 };
 
 extern "C" {
@@ -881,6 +883,7 @@ int mpcqp_ctx_destroy(mpcqp_ctx *c) {
     hipFree(c->dlist);
     hipFree(c->hbuf);
     hipFree(c->rbuf);
+    hipFree(c->fkbuf);
     hipFree(c->scratchH);
     hipFree(c->scratchF);
     if (c->ev_ok)
@@ -997,6 +1000,31 @@ static MpcArgs mpc_args(mpcqp_ctx *c, int B) {
 static int launch(const void *k, int B, size_t lds, hipStream_t s, void *arg) {
     void *args[] = {arg};
     return hip_status(hipLaunchKernel(k, dim3(B), dim3(64), args, lds, s));
+}
+
+// grow a context-owned device buffer to `bytes` (waits for the stream before freeing the old
+// one); mpcqp_ctx_reserve sizes every such buffer up front so the solve path never allocates
+static int ensure_bytes(mpcqp_ctx *c, void **buf, size_t *cap, size_t bytes) {
+    if (*cap >= bytes) return MPCQP_OK;
+    if (*buf) hipStreamSynchronize(c->stream);
+    hipFree(*buf);
+    *buf = nullptr;
+    *cap = 0;
+    if (hipMalloc(buf, bytes) != hipSuccess) return MPCQP_ERR_DEVICE;
+    *cap = bytes;
+    return MPCQP_OK;
+}
+
+static size_t host_stage_bytes(const mpcqp_ctx *c, size_t B) {
+    const size_t nx = c->m.nx, N = c->m.N, nV = (size_t)c->m.nu * c->m.N;
+    const size_t lin_w = c->m.model == MPCQP_MODEL_DENSE ? nx * (nx + c->m.nu) : 8;
+    return sizeof(double) * (nx * B + nx * (N + 1) * B + lin_w * B + nV * B + B) +
+           sizeof(uint64_t) * B + 2 * sizeof(int) * B + 64;
+}
+
+static size_t rollout_bytes(const mpcqp_ctx *c, size_t S, size_t C) {
+    const size_t B = S * C, nV = (size_t)c->m.nu * c->m.N;
+    return sizeof(double) * (B * nV + B + S * nV + S) + sizeof(int) * (2 * B + S) + 64;
 }
 
 // overflow list for B instances (grown on demand; mpcqp_ctx_reserve sizes it up front)
@@ -1132,6 +1160,7 @@ int mpcqp_batch_discretize(mpcqp_ctx *c, int B, const double *lin, double *AB) {
 static int ensure_scratch_hf(mpcqp_ctx *c, int B) {
     const size_t nV = (size_t)c->m.nu * c->m.N;
     if (c->scratch_cap >= (size_t)B) return MPCQP_OK;
+    if (c->scratchH) hipStreamSynchronize(c->stream);
     hipFree(c->scratchH);
     hipFree(c->scratchF);
     c->scratchH = c->scratchF = nullptr;
@@ -1210,16 +1239,46 @@ int mpcqp_batch_solve(mpcqp_ctx *c, int B, const double *x0, const double *xref,
         return rc;
     }
     const size_t ab = (size_t)c->m.nx * (c->m.nx + c->m.nu);
-    if (c->ab_cap < (size_t)B) {
-        hipFree(c->dAB);
-        c->dAB = nullptr;
-        c->ab_cap = 0;
-        if (hipMalloc(&c->dAB, sizeof(double) * ab * B) != hipSuccess) return MPCQP_ERR_DEVICE;
-        c->ab_cap = B;
-    }
-    int rc = mpcqp_batch_discretize(c, B, lin, c->dAB);
+    int rc = ensure_bytes(c, (void **)&c->dAB, &c->ab_cap, sizeof(double) * ab * B);
+    if (rc) return rc;
+    rc = mpcqp_batch_discretize(c, B, lin, c->dAB);
     if (rc) return rc;
     return mpcqp_batch_condense_solve(c, B, c->dAB, x0, xref, contact, U, cost, status, iters);
+}
+
+int mpcqp_ctx_reserve(mpcqp_ctx *c, int B) {
+    if (!c || B < 0) return MPCQP_ERR_BAD_ARG;
+    if (B == 0) return MPCQP_OK;
+    hipSetDevice(c->device);
+    const size_t ab = (size_t)c->m.nx * (c->m.nx + c->m.nu);
+    int rc = ensure_bytes(c, &c->hbuf, &c->hbuf_cap, host_stage_bytes(c, B));
+    if (!rc) rc = ensure_bytes(c, &c->fkbuf, &c->fkbuf_cap, sizeof(double) * 15 * (size_t)B);
+    if (!rc && c->fast && c->fk.wg) rc = ensure_list(c, B);
+    if (!rc && c->fast && c->fk.mpc_gen)
+        rc = ensure_bytes(c, &c->rbuf, &c->rbuf_cap, rollout_bytes(c, B, 1));
+    if (!rc && !c->fast) rc = ensure_bytes(c, (void **)&c->dAB, &c->ab_cap, sizeof(double) * ab * B);
+    if (!rc && !c->fast) rc = ensure_scratch_hf(c, B);
+    if (!rc) rc = hip_status(hipStreamSynchronize(c->stream));
+    return rc;
+}
+
+int mpcqp_ctx_fk_feet_host(mpcqp_ctx *c, int R, const double *q, const double *rpy,
+                           int rpy_stride, double *feet) {
+    if (!c || !q || !rpy || !feet || R < 0 || rpy_stride < 3) return MPCQP_ERR_BAD_ARG;
+    if (R == 0) return MPCQP_OK;
+    hipSetDevice(c->device);
+    const size_t nq = 6 * (size_t)R, nr = (size_t)rpy_stride * (R - 1) + 3, nf = 6 * (size_t)R;
+    if (ensure_bytes(c, &c->fkbuf, &c->fkbuf_cap, sizeof(double) * (nq + nr + nf)))
+        return MPCQP_ERR_DEVICE;
+    double *dq = (double *)c->fkbuf, *dr = dq + nq, *df = dr + nr;
+    if (hipMemcpyAsync(dq, q, sizeof(double) * nq, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemcpyAsync(dr, rpy, sizeof(double) * nr, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return MPCQP_ERR_DEVICE;
+    int rc = mpcqp_fk_feet(c->stream, R, dq, dr, rpy_stride, df);
+    if (rc) return rc;
+    if (hipMemcpyAsync(feet, df, sizeof(double) * nf, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        return MPCQP_ERR_DEVICE;
+    return hip_status(hipStreamSynchronize(c->stream));
 }
 
 int mpcqp_batch_solve_host(mpcqp_ctx *c, int B, const double *x0, const double *xref,
@@ -1233,15 +1292,7 @@ int mpcqp_batch_solve_host(mpcqp_ctx *c, int B, const double *x0, const double *
     const size_t nx = c->m.nx, N = c->m.N, nV = (size_t)c->m.nu * c->m.N;
     const size_t lin_w = c->m.model == MPCQP_MODEL_DENSE ? nx * (nx + c->m.nu) : 8;
     const size_t n_x0 = nx * B, n_xr = nx * (N + 1) * B, n_lin = lin_w * B, n_u = nV * B;
-    const size_t bytes = sizeof(double) * (n_x0 + n_xr + n_lin + n_u + B) +
-                         sizeof(uint64_t) * B + 2 * sizeof(int) * B + 64;
-    if (c->hbuf_cap < bytes) {
-        hipFree(c->hbuf);
-        c->hbuf = nullptr;
-        c->hbuf_cap = 0;
-        if (hipMalloc(&c->hbuf, bytes) != hipSuccess) return MPCQP_ERR_DEVICE;
-        c->hbuf_cap = bytes;
-    }
+    if (ensure_bytes(c, &c->hbuf, &c->hbuf_cap, host_stage_bytes(c, B))) return MPCQP_ERR_DEVICE;
     double *d_x0 = (double *)c->hbuf, *d_xr = d_x0 + n_x0, *d_lin = d_xr + n_xr,
            *d_U = d_lin + n_lin, *d_cost = d_U + n_u;
     uint64_t *d_ct = (uint64_t *)(d_cost + B);
@@ -1337,14 +1388,7 @@ int mpcqp_rollout(mpcqp_ctx *c, int S, int C, int K, double *state, double *feet
     if (S == 0 || K == 0) return MPCQP_OK;
     hipSetDevice(c->device);
     const size_t B = (size_t)S * C, nV = (size_t)c->m.nu * c->m.N;
-    const size_t bytes = sizeof(double) * (B * nV + B + S * nV + S) + sizeof(int) * (2 * B + S) + 64;
-    if (c->rbuf_cap < bytes) {
-        hipFree(c->rbuf);
-        c->rbuf = nullptr;
-        c->rbuf_cap = 0;
-        if (hipMalloc(&c->rbuf, bytes) != hipSuccess) return MPCQP_ERR_DEVICE;
-        c->rbuf_cap = bytes;
-    }
+    if (ensure_bytes(c, &c->rbuf, &c->rbuf_cap, rollout_bytes(c, S, C))) return MPCQP_ERR_DEVICE;
     double *U = (double *)c->rbuf, *cost = U + B * nV, *Ub = cost + B, *bc = Ub + S * nV;
     int *st = (int *)(bc + S), *it = st + B, *best = it + B;
     for (int k = 0; k < K; ++k) {

@@ -78,6 +78,23 @@ class BasicQPSolver {
               "mpcqp_discretize");
     }
 
+    // linear_mpc_example's own discretisation (src/linear_mpc_example.cpp:35-46): Ad = exp(Ac Ts),
+    // Bd by the 100-step quadrature, used by the mpc_test harness instead of discretizeSystem
+    void discretizeSystemQuadrature() {
+        Ad_.resize(NX_, NX_);
+        Bd_.resize(NX_, NU_);
+        check(mpcqp_discretize_quadrature(NX_, NU_, Ts_, Ac_.data(), Bc_.data(), Ad_.data(),
+                                          Bd_.data()),
+              "mpcqp_discretize_quadrature");
+    }
+
+    // mpc_test carries its own xi from (2,0,0,0) (src/linear_mpc_example.cpp:124,182); the
+    // reference QPSolver has no setter (its xi starts at zero, src/QPSolver.cpp:12)
+    template <class V0>
+    void setState(const V0 &xi) {
+        for (int i = 0; i < NX_; ++i) xi_.data()[i] = xi.data()[i];
+    }
+
     template <class V0, class M0>
     void buildQPParams(const V0 &xi0, const M0 &xi_ref, Mat &H, Vec &f, Mat &A_eq, Vec &b_eq,
                        Vec &lb, Vec &ub, Mat &A_ineq, Vec &lbA_ineq, Vec &ubA_ineq) {

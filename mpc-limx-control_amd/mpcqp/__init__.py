@@ -8,11 +8,11 @@ from ._lib import (A_COLMAJOR, A_ROWMAJOR, CONS_BOX, CONS_FRICTION, EXPORTS, LIB
                    MODEL_LITERAL, MODEL_SRBM, MPCQP_INFTY, STATUS, MpcqpError, lib)
 from .model import model_params, static_foot_offsets
 from .workload import (DEFAULT_SEED, gait_contact_mask, gait_inputs, make_batch,
-                       make_gait_states, qp_harness_inputs)
+                       make_gait_states, mpc_test_inputs, qp_harness_inputs)
 
 __all__ = [
     "A_COLMAJOR", "A_ROWMAJOR", "CONS_BOX", "CONS_FRICTION", "EXPORTS", "LIB_PATH",
     "MODEL_LITERAL", "MODEL_SRBM", "MPCQP_INFTY", "STATUS", "MpcqpError", "lib",
     "model_params", "static_foot_offsets", "DEFAULT_SEED", "gait_contact_mask", "make_batch",
-    "qp_harness_inputs", "gait_inputs", "make_gait_states",
+    "qp_harness_inputs", "mpc_test_inputs", "gait_inputs", "make_gait_states",
 ]

@@ -29,7 +29,8 @@ EXPORTS = [
     "mpcqp_batch_select_min", "mpcqp_batch_select_record", "mpcqp_reduce_records",
     "mpcqp_enable_timing", "mpcqp_last_kernel_ms",
     "mpcqp_batch_solve_gait", "mpcqp_batch_select_state", "mpcqp_batch_plant_srbm",
-    "mpcqp_rollout", "mpcqp_fk_feet", "mpcqp_kf_update",
+    "mpcqp_rollout", "mpcqp_fk_feet", "mpcqp_kf_update", "mpcqp_ctx_reserve",
+    "mpcqp_ctx_fk_feet_host",
     "mpcqp_status_string", "mpcqp_device_count",
 ]
 
@@ -89,6 +90,8 @@ def lib():
     L.mpcqp_batch_plant_srbm.argtypes = [vp, i, i] + [vp] * 5
     L.mpcqp_rollout.argtypes = [vp, i, i, i] + [vp] * 4 + [C.c_float, C.c_float, vp, vp]
     L.mpcqp_fk_feet.argtypes = [vp, i, vp, vp, i, vp]
+    L.mpcqp_ctx_fk_feet_host.argtypes = [vp, i, vp, vp, i, vp]
+    L.mpcqp_ctx_reserve.argtypes = [vp, i]
     L.mpcqp_kf_update.argtypes = [vp, i, d] + [vp] * 7
     L.mpcqp_enable_timing.argtypes = [vp, i]
     L.mpcqp_last_kernel_ms.argtypes = [vp, i]

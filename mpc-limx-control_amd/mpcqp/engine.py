@@ -62,7 +62,12 @@ class BatchEngine:
         out["iters"] = t.zeros(B, dtype=t.int32, device=dev)
         out["key"] = t.zeros(1, dtype=t.int64, device=dev)
         out["B"] = B
+        self.reserve(B)
         return out
+
+    def reserve(self, B: int):
+        """size the context's scratch for B instances: no allocation on the solve path"""
+        check("mpcqp_ctx_reserve", lib().mpcqp_ctx_reserve(self.ctx, int(B)))
 
     # -- stages ----------------------------------------------------------------------------
     def condense(self, d, H=None, f=None):

@@ -91,7 +91,8 @@ def solve_dense(H, f, A=None, lb=None, ub=None, lbA=None, ubA=None, n_wsr=0, wan
 class QPSolver:
     """Reference-compatible QPSolver (include/QPSolver.h:10-56) over the GPU C ABI."""
 
-    def __init__(self, Ts, N, Ac, Bc, Q, R, P, x_min, x_max, u_min, u_max, verbose=False):
+    def __init__(self, Ts, N, Ac, Bc, Q, R, P, x_min, x_max, u_min, u_max, verbose=False,
+                 quadrature=False):
         self.Ts, self.N = float(Ts), int(N)
         self.Ac, self.Bc = np.asarray(Ac, float), np.asarray(Bc, float)
         self.Q, self.R, self.P = (np.asarray(a, float) for a in (Q, R, P))
@@ -103,10 +104,17 @@ class QPSolver:
         self.last_status = MPCQP_OK
         self.last_iters = 0
         self.corrected = False
+        # quadrature=True: linear_mpc_example's discretisation (src/linear_mpc_example.cpp:35-46)
+        self.quadrature = bool(quadrature)
         self.discretizeSystem()
 
     def discretizeSystem(self):
-        self.Ad, self.Bd = discretize(self.Ac, self.Bc, self.Ts)
+        self.Ad, self.Bd = discretize(self.Ac, self.Bc, self.Ts, quadrature=self.quadrature)
+
+    def setState(self, xi):
+        """mpc_test carries its own xi from (2,0,0,0) (src/linear_mpc_example.cpp:124,182); the
+        reference QPSolver has no setter (its xi starts at zero, src/QPSolver.cpp:12)"""
+        self.xi = np.asarray(xi, float).reshape(self.NX).copy()
 
     def buildQPParams(self, xi0, xi_ref):
         o = build_qp(self.Ad, self.Bd, self.Q, self.R, self.P, self.x_min, self.x_max,

@@ -200,6 +200,18 @@ def qp_harness_inputs(k: int = 0):
                 u_min=-8.0, u_max=8.0, xi0=np.array([2.0, 0.0, 0.0, 0.0]), xi_ref=xr)
 
 
+def mpc_test_inputs(k: int = 0):
+    """linear_mpc_example's plant and tick-k circle reference (src/linear_mpc_example.cpp:12-33,
+    108-145): the qp_test plant written as damping / mass (-0.02 / 0.2 = -0.09999999999999999,
+    1 / 0.2 = 5), xi from (2, 0, 0, 0) carried tick to tick, t = k Ts + i Ts."""
+    h = qp_harness_inputs(k)
+    damping, mass = 0.02, 0.2
+    h["Ac"] = np.array([[0, 1, 0, 0], [0, -damping / mass, 0, 0], [0, 0, 0, 1],
+                        [0, 0, 0, -damping / mass]], float)
+    h["Bc"] = np.array([[0, 0], [1 / mass, 0], [0, 0], [0, 1 / mass]], float)
+    return h
+
+
 def make_gait_states(p: dict, S: int, seed: int = DEFAULT_SEED, candidates: int = 16):
     """Per-state data for the on-device input generation (mpcqp_batch_solve_gait), drawn
     exactly as make_batch draws them: state [S,13], feet [S,6], cmd [S,2] = (0.1 rad/s yaw

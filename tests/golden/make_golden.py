@@ -6,6 +6,7 @@ Reference (Fleming-Sung/mpc-limX-control @ 2025-04-04) restated here:
   QPSolver::buildQPParams     src/QPSolver.cpp:31-81  -> literal dense B_aug' Q_bar B_aug
   linear_mpc_example Bd       src/linear_mpc_example.cpp:35-46
   qp_test harness             src/qpSolver_test.cpp:6-90 (500-tick loop, xi-from-zero quirk)
+  mpc_test harness            src/linear_mpc_example.cpp:108-195 (quadrature Bd, xi carried)
   mpcQP::buildSystemModel     include/mpcQP.h:139-181 (literal 13x3 model)
 The reference cannot be built here (Eigen/qpOASES absent) and ships no test vectors, so these
 fixtures pin the restatements to each other and to the SURVEY.md section 8c known-answer
@@ -30,7 +31,7 @@ from scipy.optimize import linprog, minimize
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "..", "mpc-limx-control_amd"))
 from mpcqp.model import model_params  # noqa: E402  (constants only)
-from mpcqp.workload import make_batch, qp_harness_inputs  # noqa: E402  (inputs only)
+from mpcqp.workload import make_batch, mpc_test_inputs, qp_harness_inputs  # noqa: E402
 
 INF = 1e20
 
@@ -267,6 +268,30 @@ def gen_a0():
     np.savez_compressed(os.path.join(HERE, "a0_harness.npz"), **out)
 
 
+def gen_mpc_test():
+    """linear_mpc_example's 500-tick closed loop (src/linear_mpc_example.cpp:108-195): quadrature
+    Bd (:35-46), xi from (2,0,0,0) carried by xi = Ad xi + Bd u (:124,182), corrected QP per tick
+    (bounds + A_ineq rows; the stacked [A_eq; A_ineq] is infeasible)."""
+    h = mpc_test_inputs(0)
+    Ad, Bd = discretize_quadrature(h["Ac"], h["Bc"], h["Ts"])
+    N = h["N"]
+    xi = h["xi0"].copy()
+    traj, useq = [], []
+    for k in range(500):
+        hk = mpc_test_inputs(k)
+        q = build_qp(Ad, Bd, h["Q"], h["R"], h["P"], h["x_min"], h["x_max"], -8, 8, xi,
+                     hk["xi_ref"], N)
+        x, cost, kkt = qp_certified(q["H"], q["f"], q["lb"], q["ub"], q["A_ineq"], q["lbA"],
+                                    q["ubA"])
+        u = x[:2]
+        xi = Ad @ xi + Bd @ u
+        traj.append(xi.copy())
+        useq.append(u.copy())
+    np.savez_compressed(os.path.join(HERE, "mpc_test_loop.npz"), Ac=h["Ac"], Bc=h["Bc"],
+                        Ts=h["Ts"], N=N, Ad=Ad, Bd=Bd, loop_states=np.array(traj),
+                        loop_u=np.array(useq))
+
+
 def gen_srbm(config, B, keepH, seed, fname):
     p = model_params(config)
     b = make_batch(p, B, seed=seed, candidates=4)
@@ -292,9 +317,16 @@ def gen_srbm(config, B, keepH, seed, fname):
                         ub=np.array(ubs))
 
 
+GENERATORS = {
+    "a0": gen_a0,
+    "mpc_test": gen_mpc_test,
+    "B": lambda: gen_srbm("B", 24, 6, 7, "srbm_B.npz"),
+    "C": lambda: gen_srbm("C", 8, 3, 11, "srbm_C.npz"),
+    "L": lambda: gen_srbm("L", 6, 3, 13, "literal_L.npz"),
+}
+
 if __name__ == "__main__":
-    gen_a0()
-    gen_srbm("B", 24, 6, 7, "srbm_B.npz")
-    gen_srbm("C", 8, 3, 11, "srbm_C.npz")
-    gen_srbm("L", 6, 3, 13, "literal_L.npz")
+    # python make_golden.py [a0 mpc_test B C L]   (default: all)
+    for name in (sys.argv[1:] or GENERATORS):
+        GENERATORS[name]()
     print("golden fixtures written to", HERE)

@@ -30,7 +30,7 @@ def _build(name, out_dir):
 @pytest.fixture(scope="module")
 def exes(tmp_path_factory):
     d = tmp_path_factory.mktemp("cpp")
-    return {n: _build(n, d) for n in ("qp_test", "mpc_tick")}
+    return {n: _build(n, d) for n in ("qp_test", "mpc_test", "mpc_tick", "mpc_controller")}
 
 
 def test_cpp_harnesses_build(exes):
@@ -38,7 +38,7 @@ def test_cpp_harnesses_build(exes):
 
 
 def test_compat_headers_need_eigen(tmp_path):
-    for h in ("QPSolver.h", "MPCParam.h"):
+    for h in ("QPSolver.h", "MPCParam.h", "MPCController.h"):
         src = tmp_path / "t.cpp"
         src.write_text(f'#include "{os.path.join(PKG, "compat", h)}"\nint main() {{ return 0; }}\n')
         r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", str(src)], capture_output=True,
@@ -59,6 +59,22 @@ def test_cpp_qp_test_loop_matches_golden(gpu, golden, exes):
     assert len(rows) == 500
     xs = np.array([[float(v) for v in row[1:5]] for row in rows])
     assert all(row[5] == "0" and row[6] == "1" for row in rows)  # OK, corrected QP
+    np.testing.assert_allclose(xs, g["loop_states"], rtol=1e-7, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_cpp_mpc_test_loop_matches_golden(gpu, golden, exes):
+    """linear_mpc_example's loop (src/linear_mpc_example.cpp:108-195) in C++ through the
+    QPSolver mirror: quadrature Bd, xi carried from (2,0,0,0), 500 ticks vs the golden."""
+    g = golden("mpc_test_loop.npz")
+    r = subprocess.run([exes["mpc_test"], "500"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    rows = [ln.split() for ln in r.stdout.strip().splitlines()]
+    assert len(rows) == 500
+    assert all(row[7] == "0" and row[8] == "1" for row in rows)  # OK, corrected QP
+    us = np.array([[float(v) for v in row[1:3]] for row in rows])
+    xs = np.array([[float(v) for v in row[3:7]] for row in rows])
+    np.testing.assert_allclose(us, g["loop_u"], rtol=1e-7, atol=1e-9)
     np.testing.assert_allclose(xs, g["loop_states"], rtol=1e-7, atol=1e-9)
 
 
@@ -98,3 +114,99 @@ def test_cpp_convex_mpc_matches_oracle(gpu, orc, exes, tmp_path, config):
     j1 = int(np.lexsort((np.arange(C), ref1["cost"].astype(np.float32)))[0])
     assert int(tick[1]) == j1
     assert float(tick[2]) == pytest.approx(float(ref1["cost"][j1]), rel=1e-9)
+
+
+def _controller_inputs(T, seed):
+    """T ticks of (iter, odometry, joint angles) like the reference's MPC::run receives them"""
+    rng = np.random.default_rng(seed)
+    iters = rng.integers(0, 5000, size=T).astype(np.int32)
+    iters[:4] = (0, 499, 500, 999)  # gait switch boundaries of calculateGait
+    rpy = np.c_[rng.uniform(-0.1, 0.1, (T, 2)), rng.uniform(-np.pi, np.pi, T)]
+    pos = np.c_[rng.uniform(-1, 1, (T, 2)), rng.uniform(0.76, 0.86, T)]
+    quat = rng.normal(size=(T, 4))
+    quat /= np.linalg.norm(quat, axis=1, keepdims=True)
+    vel = np.c_[rng.uniform(-1, 1, T), rng.uniform(-0.3, 0.3, T), rng.normal(0, 0.05, T)]
+    omg = rng.normal(0, 0.2, (T, 3))
+    q = rng.normal(0, 0.15, (T, 6)).astype(np.float32)
+    return iters, pos, rpy, quat, vel, omg, q
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("literal,ncand", [(0, 1), (1, 1), (0, 4)])
+def test_cpp_mpc_controller_tick_matches_oracle(gpu, orc, exes, tmp_path, literal, ncand):
+    """MPC::run (include/MPCController.h:183-196) with the support-force QP filled in
+    (mpcqp::BasicMPC, what compat/MPCController.h instantiates), driven with test-only limxsdk /
+    estimator stand-ins: gait state, foot placement, x0 / xref (include/mpcQP.h:66-97), lever
+    arms from the FK kernel, the horizon contact schedule and the chosen plan's first-step forces
+    all match a restatement built on the oracle (FK, gait mask, SRBM condense + solve)."""
+    import mpcqp
+    N, T = 20, 12
+    p = mpcqp.model_params("B", N=N)
+    iters, pos, rpy, quat, vel, omg, q = _controller_inputs(T, 4242 + literal + ncand)
+    f = tmp_path / "ticks.bin"
+    with open(f, "wb") as fh:
+        for t in range(T):
+            fh.write(np.int32(iters[t]).tobytes())
+            od = np.concatenate([pos[t], rpy[t], quat[t], vel[t], omg[t]]).astype("<f8")
+            fh.write(od.tobytes())
+            fh.write(q[t].astype("<f4").tobytes())
+    r = subprocess.run([exes["mpc_controller"], str(N), str(T), str(literal), str(ncand), str(f)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    rows = [ln.split() for ln in r.stdout.strip().splitlines()]
+    assert len(rows) == T
+    left_off, right_off = mpcqp.static_foot_offsets()
+    Ts = p["Ts"]
+    for t, row in enumerate(rows):
+        tok = {}
+        key = None
+        for w in row:
+            if w in ("tick", "gait", "place", "x0", "xref", "lin", "contact", "choice", "status",
+                     "cost", "force"):
+                key = w
+                tok[key] = []
+            else:
+                tok[key].append(w)
+        # calculateGait, include/MPCController.h:61-75 (float time, as the reference)
+        now = np.float32(iters[t]) * np.float32(0.001)
+        ph = float(np.fmod(float(now), float(np.float32(0.5) + np.float32(0.5))))
+        lft = 1 if ph < 0.5 else 0
+        remain = (0.5 - ph) if lft else (1.0 - ph)
+        assert [int(tok["gait"][0]), int(tok["gait"][1])] == [lft, 1 - lft]
+        assert float(tok["gait"][2]) == ph and abs(float(tok["gait"][3]) - remain) < 1e-15
+        # computeFootPlacement, :106-132 (desieredV_pos = (1, 0, 0))
+        off = left_off if lft else right_off
+        assert abs(float(tok["place"][0]) - (pos[t, 0] + remain + 0.25 + off[0])) < 1e-14
+        assert abs(float(tok["place"][1]) - (pos[t, 1] + off[1])) < 1e-14
+        # x0 / xref, include/mpcQP.h:66-97
+        x0 = np.concatenate([rpy[t], pos[t], omg[t], vel[t], [-9.8]])
+        xr = np.zeros((N + 1, 13))
+        for i in range(N + 1):
+            tt = i * Ts
+            xr[i] = np.concatenate([[rpy[t, 0], rpy[t, 1], rpy[t, 2] + tt * 0.1,
+                                     pos[t, 0] + tt * 0.5, pos[t, 1], pos[t, 2]], omg[t],
+                                    [vel[t, 0] if i == 0 else 0.5, vel[t, 1], vel[t, 2], -9.8]])
+        np.testing.assert_array_equal(np.array(tok["x0"], float), x0)
+        np.testing.assert_array_equal(np.array(tok["xref"], float), xr.reshape(-1))
+        # lever arms from FK (GPU kernel vs the oracle's chain)
+        qd = q[t].astype(np.float64)
+        if literal:
+            feet = orc.fk_feet(qd, np.zeros(3)) - np.tile(pos[t], 2)
+        else:
+            feet = orc.fk_feet(qd, rpy[t])
+        lin = np.concatenate([[rpy[t, 2]], feet, [0.0]])
+        np.testing.assert_allclose(np.array(tok["lin"], float), lin, rtol=0, atol=1e-13)
+        # horizon schedules: the reference's gait plus candidate offsets
+        masks = np.array([orc.gait_contact_mask(N, Ts, float(now) + 0.0625 * c) for c in
+                          range(ncand)], dtype=np.uint64)
+        lin_gpu = np.array(tok["lin"], float)
+        ref = orc.srbm_batch(p, np.repeat(x0[None], ncand, 0), np.repeat(xr.reshape(1, -1), ncand, 0),
+                             np.repeat(lin_gpu[None], ncand, 0), masks)
+        assert np.all(ref["status"] == 0)
+        j = int(np.lexsort((np.arange(ncand), ref["cost"].astype(np.float32)))[0])
+        assert int(tok["choice"][0]) == j and int(tok["status"][0]) == 0
+        assert int(tok["contact"][0]) == int(masks[j])
+        assert float(tok["cost"][0]) == pytest.approx(float(ref["cost"][j]), rel=1e-9)
+        U0 = np.array(tok["force"], float)
+        np.testing.assert_allclose(U0, ref["U"][j][:6], rtol=0,
+                                   atol=1e-8 * max(1.0, np.abs(ref["U"][j]).max()))

@@ -117,6 +117,33 @@ def test_qpsolver_class_closed_loop(gpu, golden):
     np.testing.assert_allclose(xi, g["loop_states"][99], rtol=1e-7, atol=1e-9)
 
 
+def test_qpsolver_mpc_test_closed_loop(gpu, golden):
+    """mpc_test (src/linear_mpc_example.cpp:108-195) through the QPSolver mirror: quadrature
+    Bd (mpcqp_discretize_quadrature), xi carried from (2,0,0,0), the stacked [A_eq; A_ineq] the
+    harness builds (corrected on the GPU), 500 ticks against the certified trajectory."""
+    from mpcqp.qpsolver import QPSolver
+    import mpcqp
+    g = golden("mpc_test_loop.npz")
+    h = mpcqp.mpc_test_inputs(0)
+    qp = QPSolver(h["Ts"], h["N"], h["Ac"], h["Bc"], h["Q"], h["R"], h["P"], h["x_min"],
+                  h["x_max"], h["u_min"], h["u_max"], quadrature=True)
+    np.testing.assert_allclose(qp.Bd, g["Bd"], rtol=0, atol=1e-14)
+    xi = h["xi0"].copy()
+    qp.setState(xi)
+    for k in range(500):
+        hk = mpcqp.mpc_test_inputs(k)
+        H, f, A_eq, b_eq, lb, ub, A_ineq, lbA, ubA = qp.buildQPParams(xi, hk["xi_ref"])
+        A_total = np.vstack([A_eq, A_ineq])
+        ok, U_opt = qp.solveQP(H, f, A_total, lb, ub, np.concatenate([b_eq, lbA]),
+                               np.concatenate([b_eq, ubA]))
+        assert ok and qp.corrected and qp.last_status == 0
+        qp.updateState(U_opt[:, 0])
+        xi = qp.getState()
+        if k in (0, 99, 250, 499):
+            np.testing.assert_allclose(U_opt[:, 0], g["loop_u"][k], rtol=1e-7, atol=1e-9)
+            np.testing.assert_allclose(xi, g["loop_states"][k], rtol=1e-7, atol=1e-9)
+
+
 # ------------------------------------------------------------------------- batched engine
 def run_batch(p, batch, want_hf=False, expect_fast=True):
     """fused fast path (discretize + condense_solve); with want_hf also the generic path

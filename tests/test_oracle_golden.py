@@ -171,3 +171,27 @@ def test_expm_all_pade_degrees(orc, scale):
     A = rng.normal(size=(7, 7))
     A *= scale / np.abs(A).sum(0).max()
     assert rel_err(orc.expm(A), sl.expm(A)) <= 1e-12
+
+
+def test_mpc_test_closed_loop(golden, orc):
+    """linear_mpc_example's 500-tick loop (src/linear_mpc_example.cpp:108-195): the oracle's
+    quadrature Bd (:35-46) against the fixture's scipy one, xi carried from (2,0,0,0) by
+    xi = Ad xi + Bd u (:124,182), corrected QP per tick, against the certified trajectory."""
+    g = golden("mpc_test_loop.npz")
+    import mpcqp
+    h = mpcqp.mpc_test_inputs(0)
+    Ad, Bd = orc.discretize(h["Ac"], h["Bc"], h["Ts"], quadrature=True)
+    np.testing.assert_allclose(Ad, g["Ad"], rtol=0, atol=1e-14)
+    np.testing.assert_allclose(Bd, g["Bd"], rtol=0, atol=1e-14)
+    N = int(g["N"])
+    xi = h["xi0"].copy()
+    for k in range(500):
+        hk = mpcqp.mpc_test_inputs(k)
+        o = orc.build_qp(Ad, Bd, h["Q"], h["R"], h["P"], h["x_min"], h["x_max"], -8, 8, xi,
+                         hk["xi_ref"], N)
+        st, U, *_ = orc.solve_qp(o["H"], o["f"], o["lb"], o["ub"], o["A_ineq"], o["lbA"], o["ubA"])
+        assert st == 0
+        xi = Ad @ xi + Bd @ U[:2]
+        if k in (0, 99, 499):
+            np.testing.assert_allclose(U[:2], g["loop_u"][k], rtol=1e-7, atol=1e-9)
+            np.testing.assert_allclose(xi, g["loop_states"][k], rtol=1e-7, atol=1e-9)
