@@ -1,0 +1,172 @@
+// chol_mfma.hpp -- blocked Cholesky H_FF = L L' and triangular inverse X = L^-1 of ONE QP's
+// reduced Hessian on the FP64 matrix cores (v_mfma_f64_16x16x4_f64), for the workgroup
+// solvers (gi_wg.hpp: the whole-body configuration E and the double-support / standing
+// overflow).  The Goldfarb-Idnani start needs J = L^-T and t = L^-1 g (qpOASES's dense
+// factorisation in QPSolver::solveQP, src/QPSolver.cpp:87-96); column-by-column sweeps cost one
+// workgroup barrier and one LDS broadcast per column, this costs three barriers per 16 columns.
+//
+// Storage (LDS, per QP): the lower triangle as 16 x 16 tiles, tile (i, j) at TS * tix(i, j).
+// A stored tile S is kept in the matrix cores' C/D order ("slices"): element (a, b) of S at
+// 64 (a >> 2) + 16 (a & 3) + b, so slice s read at offset 64 s + lane is the accumulator
+// register s of an MFMA result (lane l: row (l >> 4) + 4 s, column l & 15), the B operand of
+// step s (k = (l >> 4) + 4 s, column l & 15) of S, and the A operand of step s of S' -- every
+// operand below is one conflict-free ds_read_b64 at the same offset:
+//   H / L tiles (i > j) store their TRANSPOSE (S = L_ij'),  X tiles store X_ij itself,
+//   the diagonal tile k ends up holding W_k = L_kk^-1 (= X_kk), Wt[k] holds W_k'.
+// Algorithm (T = NF / 16 block columns):
+//   for k:  W_k = (chol of tile k)^-1 on wave 0 (16 lanes, registers)        | barrier
+//           L_ik' = W_k H_ik'                (A = W_k, B = H_ik', 4 MFMAs)    | barrier
+//           H_ij' -= L_jk L_ik'  (k < j <= i)(A = L_jk, B = L_ik', 4 MFMAs)   | barrier
+//   for i:  X_ij = -W_i sum_{m=j}^{i-1} L_im X_mj  (j < i; the sum's accumulator is the B
+//           operand of the W_i product in place)                              | 2 barriers
+// Tiles of one step are spread round-robin over the workgroup's waves.
+#pragma once
+#include "mfma_ops.hpp"
+
+namespace mpcqp {
+
+template <int NF>
+struct TileFact {
+    static_assert(NF % 16 == 0, "16-column blocks");
+    static constexpr int T = NF / 16;
+    static constexpr int TS = 272;  // 256 + 16: tiles (i, j) and (i, j + 1) sit 16 bank pairs apart
+    static constexpr int NT = T * (T + 1) / 2;
+    static constexpr int oTiles = 0;
+    static constexpr int oWt = NT * TS;        // W_k' slices
+    static constexpr int oG = oWt + T * TS;    // g
+    static constexpr int oFlag = oG + NF;      // non-PD flag
+    static constexpr int doubles = oFlag + 2;
+    // X (c, r): row c, column r of X = L^-1 (c >= r) -- J(r, c)
+    static __device__ __forceinline__ int xoff(int c, int r) {
+        const int i = c >> 4, j = r >> 4, a = c & 15;
+        return TS * (i * (i + 1) / 2 + j) + 64 * (a >> 2) + 16 * (a & 3) + (r & 15);
+    }
+};
+
+__device__ __forceinline__ int tix(int i, int j) { return i * (i + 1) / 2 + j; }
+
+// Cholesky of the 16 x 16 block in `tile` (lower triangle of the stored S = H_kk', i.e. of H_kk
+// as it is symmetric) and W = L^-1, on lanes 0..15 of the calling wave: lane i owns row i of L,
+// then lane c column c of W.  Writes W's slices over the tile and W' slices to wt.
+__device__ __forceinline__ void diag_block_inverse(double *tile, double *wt, bool &bad) {
+    const int ln = lane();
+    const bool on = ln < 16;
+    const int li = ln & 15;
+    double a[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+        a[j] = (on && j <= li) ? tile[64 * (li >> 2) + 16 * (li & 3) + j] : 0.0;
+    double iq[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const double piv = readlane(a[k], k);
+        bad |= !(piv > 0.0);
+        const double isq = rsqrt_nr(piv);
+        iq[k] = isq;
+        const double lk = a[k] * isq;  // L(ln, k); on lane k, L(k, k) = piv / sqrt(piv)
+        a[k] = lk;
+#pragma unroll
+        for (int j = k + 1; j < 16; ++j) {
+            const double ljk = readlane(lk, j);
+            if (li > k) a[j] -= lk * ljk;
+        }
+    }
+    // W = L^-1, lane c: column c by forward substitution (L entries are wave-uniform)
+    double w[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        double s = (li == i) ? 1.0 : 0.0;
+#pragma unroll
+        for (int m = 0; m < i; ++m) s -= readlane(a[m], i) * w[m];
+        w[i] = s * iq[i];
+    }
+    if (on) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            tile[64 * (i >> 2) + 16 * (i & 3) + li] = w[i];   // W(i, c), c = li
+            wt[64 * (li >> 2) + 16 * (li & 3) + i] = w[i];    // W'(c, i)
+        }
+    }
+}
+
+// Blocked factorisation + inverse of the NF x NF matrix whose tiles are in F (TileFact layout),
+// by the workgroup's NW waves (wave index wv).  Returns the non-PD flag (same on every thread).
+template <int NF, int NW>
+__device__ __forceinline__ bool chol_inverse_mfma(double *F, int wv) {
+    using TF = TileFact<NF>;
+    constexpr int T = TF::T, TS = TF::TS;
+    const int ln = lane();
+    double *tiles = F + TF::oTiles, *Wt = F + TF::oWt;
+    bool bad = false;
+    for (int k = 0; k < T; ++k) {
+        if (wv == 0) {
+            diag_block_inverse(tiles + TS * tix(k, k), Wt + TS * k, bad);
+            if (ln == 0 && bad) F[TF::oFlag] = 1.0;
+        }
+        __syncthreads();
+        // panel: L_ik' = W_k H_ik'
+        for (int i = k + 1 + wv; i < T; i += NW) {
+            const double *wk = Wt + TS * k;
+            double *ti = tiles + TS * tix(i, k);
+            dx4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(wk[64 * s + ln], ti[64 * s + ln], acc, 0, 0, 0);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) ti[64 * s + ln] = acc[s];
+        }
+        __syncthreads();
+        // trailing update: H_ij' -= L_jk L_ik', k < j <= i (pairs in row-major order)
+        const int np = (T - 1 - k) * (T - k) / 2;
+        for (int t = wv; t < np; t += NW) {
+            int i = k + 1, rem = t;
+            while (rem >= i - k) { rem -= i - k; ++i; }
+            const int j = k + 1 + rem;
+            const double *lj = tiles + TS * tix(j, k), *li = tiles + TS * tix(i, k);
+            double *c = tiles + TS * tix(i, j);
+            dx4 acc = {c[ln], c[64 + ln], c[128 + ln], c[192 + ln]};
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-lj[64 * s + ln], li[64 * s + ln], acc, 0, 0, 0);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) c[64 * s + ln] = acc[s];
+        }
+        __syncthreads();
+    }
+    // X = L^-1 below the diagonal, block row by block row
+    constexpr int MAXJ = (T - 1 + NW - 1) / NW;
+    for (int i = 1; i < T; ++i) {
+        dx4 xr[MAXJ > 0 ? MAXJ : 1];
+#pragma unroll
+        for (int u = 0; u < MAXJ; ++u) {
+            const int j = wv + u * NW;
+            if (j >= i) break;
+            dx4 q = {0.0, 0.0, 0.0, 0.0};
+            for (int m = j; m < i; ++m) {
+                const double *lim = tiles + TS * tix(i, m), *xmj = tiles + TS * tix(m, j);
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+                    q = __builtin_amdgcn_mfma_f64_16x16x4f64(lim[64 * s + ln], xmj[64 * s + ln], q, 0, 0, 0);
+            }
+            const double *wi = Wt + TS * i;
+            dx4 x = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+                x = __builtin_amdgcn_mfma_f64_16x16x4f64(-wi[64 * s + ln], q[s], x, 0, 0, 0);
+            xr[u] = x;
+        }
+        __syncthreads();  // every read of L_i* is done before X_i* overwrites it
+#pragma unroll
+        for (int u = 0; u < MAXJ; ++u) {
+            const int j = wv + u * NW;
+            if (j >= i) break;
+            double *c = tiles + TS * tix(i, j);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) c[64 * s + ln] = xr[u][s];
+        }
+        __syncthreads();
+    }
+    return F[TF::oFlag] != 0.0;
+}
+
+}  // namespace mpcqp

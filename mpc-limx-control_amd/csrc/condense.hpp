@@ -178,6 +178,9 @@ __device__ __forceinline__ void alg_comb(int nx, int ns, double *out, const doub
     wave_sync();
 }
 
+__device__ __forceinline__ void expm_pade_solve(int nx, int ns, const double *U, const double *V,
+                                                double *D, double *E);
+
 // E = exp([[A, B],[0, 0]]) top block, A = T (nx x ns, already scaled by Ts), Eigen's degree
 // selection.  ws: 7 * nx * ns doubles of scratch.  Result written to E (nx x ns).
 __device__ __forceinline__ void wave_expm(int nx, int ns, double *T, double *ws, double *E) {
@@ -257,9 +260,22 @@ __device__ __forceinline__ void wave_expm(int nx, int ns, double *T, double *ws,
         b0 = b[0];
     }
     (void)b0;
-    // numer = U + V (scalar b0), denom = -U + V (scalar b0).  Solve denom X = numer:
-    //   X = [D1^-1 N1, D1^-1 (N2 - D2)]  (bottom block of X is I).
-    double *D = A2, *X = E;
+    expm_pade_solve(nx, ns, U, V, A2, E);
+    // squarings: (E,1)^2 = [E1 E1, E1 E2 + E2]
+    for (int s = 0; s < squarings; ++s) {
+        alg_mul(nx, ns, E, E, 1.0, W);
+        for (int e = lane(); e < sz; e += kWave) E[e] = W[e];
+        wave_sync();
+    }
+}
+
+// The Pade quotient of wave_expm: numer = U + V (scalar b0), denom = -U + V (scalar b0).
+// Solve denom X = numer:  X = [D1^-1 N1, D1^-1 (N2 - D2)]  (bottom block of X is I).
+// One wave; D (nx x ns scratch), X = E (nx x ns).
+__device__ __forceinline__ void expm_pade_solve(int nx, int ns, const double *U, const double *V,
+                                                double *D, double *E) {
+    const int sz = nx * ns;
+    double *X = E;
     for (int e = lane(); e < sz; e += kWave) {
         const double n = U[e] + V[e], d = -U[e] + V[e];
         D[e] = d;
@@ -309,12 +325,6 @@ __device__ __forceinline__ void wave_expm(int nx, int ns, double *T, double *ws,
             X[j * nx + i] = s / D[i * nx + i];
         }
     wave_sync();
-    // squarings: (E,1)^2 = [E1 E1, E1 E2 + E2]
-    for (int s = 0; s < squarings; ++s) {
-        alg_mul(nx, ns, E, E, 1.0, W);
-        for (int e = lane(); e < sz; e += kWave) E[e] = W[e];
-        wave_sync();
-    }
 }
 
 // Horizon condensing.  AB = [Ad | Bd] (nx x ns).  ws must hold

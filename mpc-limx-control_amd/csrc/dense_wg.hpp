@@ -3,7 +3,8 @@
 // workgroup per QP:
 //
 //   discretisation   [Ad | Bd] = top block of exp([[Ac, Bc], [0, 0]] Ts): Eigen's Pade degree
-//                    selection + scaling and squaring (wave_expm, condense.hpp)
+//                    selection + scaling and squaring (wg_expm, expm_wg.hpp: the products on
+//                    the matrix cores over the workgroup)
 //                                                            QPSolver::discretizeSystem,
 //                                                            src/QPSolver.cpp:21-29
 //   condensing       H = 2 (B'QB + R), f = 2 B'Q (A x0 - xref)   QPSolver::buildQPParams,
@@ -23,6 +24,7 @@
 // stored.  Per instance: [Ac | Bc] (NX x NS), x0, xref in; U, cost, status, iterations out.
 #pragma once
 #include "condense.hpp"
+#include "expm_wg.hpp"
 #include "gi_wg.hpp"
 #include "mfma_ops.hpp"
 #include "mpc_fused.hpp"
@@ -60,7 +62,7 @@ struct DenseLayout {
     static_assert(LS * NV <= 3 * LD * NX, "the staged M tile fits the Z region");
     static constexpr int nFront = oR - oU + (nExpm > nCond ? nExpm : nCond);
     // solver view (after every thread holds its H_FF row part and g)
-    static constexpr int nSolver = WgLayout<NF>::doubles;
+    static constexpr int nSolver = WgLayout<NF>::work;
     static constexpr int nDoubles = oU + (nFront > nSolver ? nFront : nSolver);
     static constexpr size_t bytes =
         sizeof(double) * nDoubles + sizeof(int) * (NF + NV) + ((MT + 15) & ~15);
@@ -118,9 +120,9 @@ __device__ __forceinline__ void dense_mpc_one(const MpcArgs &a, int b, unsigned 
         for (int e = tid; e < NX * (N + 1); e += NT) xr[e] = xrg[e];
     }
     __syncthreads();
-    // ---- discretisation (wave 0) and the free map / bounds
+    // ---- discretisation (the workgroup, matrix cores) and the free map / bounds (wave 0)
+    wg_expm(NX, NS, D + Lay::oT, D + Lay::oWs, AB, tid, NT, wv, NT / 64);
     if (wv == 0) {
-        wave_expm(NX, NS, D + Lay::oT, D + Lay::oWs, AB);
         gi_setup(C);
         if (C.nf > a.max_free) C.status = ST_BAD_DIMS;
         if (ln == 0) {

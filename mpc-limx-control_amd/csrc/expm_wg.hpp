@@ -1,0 +1,140 @@
+// expm_wg.hpp -- wave_expm (condense.hpp: Eigen's Pade degree selection and scaling and
+// squaring of exp([[A, B], [0, 0]] Ts), QPSolver::discretizeSystem, src/QPSolver.cpp:21-29) run by
+// a whole workgroup: the (top block, scalar) algebra products go to the FP64 matrix cores as
+// 16 x 16 output tiles spread over the waves, the linear combinations over every thread; the
+// Pade quotient's partial-pivot LU stays on one wave (expm_pade_solve).  Same operations and
+// branch thresholds as wave_expm; products differ from it only in summation order.
+#pragma once
+#include "condense.hpp"
+#include "mfma_ops.hpp"
+
+namespace mpcqp {
+
+// out = X * Y in the top-block algebra (alg_mul): out[:, j] = X1 Y[:, j] (+ sY X[:, j], j >= nx)
+__device__ __forceinline__ void wg_alg_mul(int nx, int ns, const double *X, const double *Y,
+                                           double sY, double *out, int wv, int nw) {
+    const int tm_n = (nx + 15) >> 4, tn_n = (ns + 15) >> 4, ks = (nx + 3) >> 2;
+    const int ln = lane(), li = ln & 15, lk = ln >> 4;
+    for (int t = wv; t < tm_n * tn_n; t += nw) {
+        const int tm = t % tm_n, tn = t / tm_n;
+        const int i = tm * 16 + li, j = tn * 16 + li;
+        dx4 acc = {0.0, 0.0, 0.0, 0.0};
+        for (int s = 0; s < ks; ++s) {
+            const int kk = 4 * s + lk;
+            const bool kin = kk < nx;
+            const double a = (i < nx && kin) ? X[kk * nx + i] : 0.0;
+            const double b = (j < ns && kin) ? Y[j * nx + kk] : 0.0;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = tm * 16 + lk + 4 * r, col = tn * 16 + li;
+            if (row < nx && col < ns) {
+                double v = acc[r];
+                if (col >= nx) v += sY * X[col * nx + row];
+                out[col * nx + row] = v;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// out = sum_q c[q] M[q] + cI I (alg_comb) over every thread
+template <int K>
+__device__ __forceinline__ void wg_alg_comb(int nx, int ns, double *out, const double (&c)[K],
+                                            const double *const (&M)[K], double cI, int tid,
+                                            int nt) {
+    for (int e = tid; e < nx * ns; e += nt) {
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) s += c[q] * M[q][e];
+        const int i = e % nx, j = e / nx;
+        if (i == j) s += cI;
+        out[e] = s;
+    }
+    __syncthreads();
+}
+
+// wave_expm by the workgroup (nt threads, nw waves).  T (nx x ns, scaled by Ts) is overwritten
+// when scaling; ws: 7 nx ns doubles; E: the result top block.  Every thread must call it.
+__device__ __forceinline__ void wg_expm(int nx, int ns, double *T, double *ws, double *E, int tid,
+                                        int nt, int wv, int nw) {
+    const int sz = nx * ns;
+    double *A2 = ws, *A4 = ws + sz, *A6 = ws + 2 * sz, *A8 = ws + 3 * sz, *U = ws + 4 * sz,
+           *V = ws + 5 * sz, *W = ws + 6 * sz;
+    double cs = 0.0;  // 1-norm, computed by every wave alike
+    for (int j = lane(); j < ns; j += kWave) {
+        double s = 0.0;
+        for (int i = 0; i < nx; ++i) s += fabs(T[j * nx + i]);
+        cs = fmax(cs, s);
+    }
+    const double l1 = wave_max(cs);
+    int squarings = 0;
+    if (l1 < 1.495585217958292e-002) {
+        const double b[] = {120., 60., 12., 1.};
+        wg_alg_mul(nx, ns, T, T, 0.0, A2, wv, nw);
+        wg_alg_comb<1>(nx, ns, W, {b[3]}, {A2}, b[1], tid, nt);
+        wg_alg_mul(nx, ns, T, W, b[1], U, wv, nw);
+        wg_alg_comb<1>(nx, ns, V, {b[2]}, {A2}, b[0], tid, nt);
+    } else if (l1 < 2.539398330063230e-001) {
+        const double b[] = {30240., 15120., 3360., 420., 30., 1.};
+        wg_alg_mul(nx, ns, T, T, 0.0, A2, wv, nw);
+        wg_alg_mul(nx, ns, A2, A2, 0.0, A4, wv, nw);
+        wg_alg_comb<2>(nx, ns, W, {b[5], b[3]}, {A4, A2}, b[1], tid, nt);
+        wg_alg_mul(nx, ns, T, W, b[1], U, wv, nw);
+        wg_alg_comb<2>(nx, ns, V, {b[4], b[2]}, {A4, A2}, b[0], tid, nt);
+    } else if (l1 < 9.504178996162932e-001) {
+        const double b[] = {17297280., 8648640., 1995840., 277200., 25200., 1512., 56., 1.};
+        wg_alg_mul(nx, ns, T, T, 0.0, A2, wv, nw);
+        wg_alg_mul(nx, ns, A2, A2, 0.0, A4, wv, nw);
+        wg_alg_mul(nx, ns, A4, A2, 0.0, A6, wv, nw);
+        wg_alg_comb<3>(nx, ns, W, {b[7], b[5], b[3]}, {A6, A4, A2}, b[1], tid, nt);
+        wg_alg_mul(nx, ns, T, W, b[1], U, wv, nw);
+        wg_alg_comb<3>(nx, ns, V, {b[6], b[4], b[2]}, {A6, A4, A2}, b[0], tid, nt);
+    } else if (l1 < 2.097847961257068e+000) {
+        const double b[] = {17643225600., 8821612800., 2075673600., 302702400., 30270240.,
+                            2162160.,     110880.,     3960.,       90.,        1.};
+        wg_alg_mul(nx, ns, T, T, 0.0, A2, wv, nw);
+        wg_alg_mul(nx, ns, A2, A2, 0.0, A4, wv, nw);
+        wg_alg_mul(nx, ns, A4, A2, 0.0, A6, wv, nw);
+        wg_alg_mul(nx, ns, A6, A2, 0.0, A8, wv, nw);
+        wg_alg_comb<4>(nx, ns, W, {b[9], b[7], b[5], b[3]}, {A8, A6, A4, A2}, b[1], tid, nt);
+        wg_alg_mul(nx, ns, T, W, b[1], U, wv, nw);
+        wg_alg_comb<4>(nx, ns, V, {b[8], b[6], b[4], b[2]}, {A8, A6, A4, A2}, b[0], tid, nt);
+    } else {
+        const double maxnorm = 5.371920351148152;
+        frexp(l1 / maxnorm, &squarings);
+        if (squarings < 0) squarings = 0;
+        __syncthreads();  // every wave has read T for its norm
+        for (int e = tid; e < sz; e += nt) T[e] = ldexp(T[e], -squarings);
+        __syncthreads();
+        const double b[] = {64764752532480000., 32382376266240000., 7771770303897600.,
+                            1187353796428800.,  129060195264000.,   10559470521600.,
+                            670442572800.,      33522128640.,       1323241920.,
+                            40840800.,          960960.,            16380.,
+                            182.,               1.};
+        wg_alg_mul(nx, ns, T, T, 0.0, A2, wv, nw);
+        wg_alg_mul(nx, ns, A2, A2, 0.0, A4, wv, nw);
+        wg_alg_mul(nx, ns, A4, A2, 0.0, A6, wv, nw);
+        wg_alg_comb<3>(nx, ns, V, {b[13], b[11], b[9]}, {A6, A4, A2}, 0.0, tid, nt);
+        wg_alg_mul(nx, ns, A6, V, 0.0, W, wv, nw);
+        wg_alg_comb<3>(nx, ns, A8, {b[7], b[5], b[3]}, {A6, A4, A2}, b[1], tid, nt);
+        for (int e = tid; e < sz; e += nt) W[e] += A8[e];
+        __syncthreads();
+        wg_alg_mul(nx, ns, T, W, b[1], U, wv, nw);
+        wg_alg_comb<3>(nx, ns, W, {b[12], b[10], b[8]}, {A6, A4, A2}, 0.0, tid, nt);
+        wg_alg_mul(nx, ns, A6, W, 0.0, V, wv, nw);
+        wg_alg_comb<3>(nx, ns, A8, {b[6], b[4], b[2]}, {A6, A4, A2}, b[0], tid, nt);
+        for (int e = tid; e < sz; e += nt) V[e] += A8[e];
+        __syncthreads();
+    }
+    if (wv == 0) expm_pade_solve(nx, ns, U, V, A2, E);
+    __syncthreads();
+    for (int s = 0; s < squarings; ++s) {
+        wg_alg_mul(nx, ns, E, E, 1.0, W, wv, nw);
+        for (int e = tid; e < sz; e += nt) E[e] = W[e];
+        __syncthreads();
+    }
+}
+
+}  // namespace mpcqp

@@ -7,17 +7,11 @@
 // Same algorithm, constraint order and tolerances as gi_run_reg (gi_reg.hpp), gi_run
 // (gi_solver.hpp) and the CPU oracle; only the distribution over threads differs:
 //   * 256 threads = rows 0..127 x two column halves.  Thread (r, h) (h = tid / 128, waves 0-1
-//     are half 0, waves 2-3 half 1) holds columns [h NF/2, (h+1) NF/2) of row r: first of H_FF
-//     (then L, right-looking Cholesky), then of J = L^-T Q.  NF/2 <= 64 doubles per thread.
-//   * Cholesky: step k publishes column k (and g_k) to LDS, one barrier, every thread updates
-//     its part of row r.  For the factorisation the columns are interleaved over the halves
-//     (even columns in half 0, odd in half 1), so after each pair of steps both halves drop
-//     their first slot together: the published column is always slot 0 (runtime loop,
-//     compile-time register indices).  L is parked in LDS (column-major packed) and g rides
-//     along (t = L^-1 g).
-//   * J = L^-T by back substitution of L' J = I, one row per step: the owner of row l scales
-//     and publishes it, every row r < l subtracts L(l, r) times it.  The two halves are
-//     independent here (each column of J is its own system).
+//     are half 0, waves 2-3 half 1) hands in row r of H_FF (columns 2j + h <= r) and holds
+//     columns [h NF/2, (h+1) NF/2) of row r of J = L^-T Q.  NF/2 <= 64 doubles per thread.
+//   * Cholesky and J = L^-T: the blocked FP64-MFMA factorisation and triangular inverse of
+//     chol_mfma.hpp on 16 x 16 tiles in LDS (three barriers per 16 columns), then every thread
+//     reads its J row part (J(r, c) = X(c, r), X = L^-1) and t = L^-1 g = X g.
 //   * Dual loop: the most violated constraint is found by the rows of half 0 (bounds of their
 //     own variable and, for a foot's vertical force, that foot-step's friction rows); the
 //     constraint's normal n is published as J rows (d = J' n); z = J2 d2 is a per-half dot
@@ -28,6 +22,7 @@
 //   * Sums across threads are combined in a fixed order (half 0 + half 1, wave 0 + wave 1),
 //     so both halves hold bit-identical copies of x, z and every scalar.
 #pragma once
+#include "chol_mfma.hpp"
 #include "gi_reg.hpp"
 
 namespace mpcqp {
@@ -63,6 +58,8 @@ struct WgLayout {
     static constexpr int oAct = oRed + 32;           // slot constraint ids (int)
     static constexpr int doubles = oAct + RW / 2;
     static_assert(2 * CBW >= 2 * NF, "rotations fit the column buffers");
+    // the blocked factorisation (chol_mfma.hpp) overlays the whole workspace before the loop
+    static constexpr int work = doubles > TileFact<NF>::doubles ? doubles : TileFact<NF>::doubles;
 };
 
 struct WgIds {
@@ -127,86 +124,45 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
     double Jr[NH];
     MPCQP_STAMP_INIT(tst);
 
-    // ---- Cholesky H_FF = L L' (right-looking) with the forward solve L t = g in the same sweep
+    // ---- H_FF = L L' and X = L^-1 on the matrix cores (chol_mfma.hpp), tiles in LDS over the
+    //      workspace; then J(r, c) = X(c, r) (c >= r) and t = X g per row
     double gv = (live && r < nf) ? g : 0.0;
     if (status == ST_OK && nf > 0) {
-        bool bad = false;
-        // Columns are interleaved over the halves for the factorisation (hr[j] of half h is
-        // column 2(m + j) + h after m super-steps): super-step m eliminates column 2m (owned
-        // by half 0, its slot 0) and then column 2m + 1 (half 1, slot 0), after which both
-        // halves shift their arrays by one.  Both halves run the same straight-line code, the
-        // published column is always slot 0 (compile-time register indices, runtime loop).
-        const int npair = (nf + 1) >> 1;
-        for (int m = 0; m < npair; ++m) {
+        using TF = TileFact<NF>;
+        constexpr int TS = TF::TS;
+        double *F = W;
+        if (live) {
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int k = 2 * m + e;
-                if (k >= nf) break;
-                double *cb = colb + e * CBW;
-                if (h == e && live && r >= k) cb[r] = hr[0];   // column k (pivot at r == k)
-                if (tid == k) cb[RW] = gv;                      // g_k (thread (k, 0))
-                __syncthreads();
-                const double piv = cb[k];
-                bad |= !(piv > 0.0);
-                const double isq = rsqrt_nr(piv);               // 1 / L(k,k)
-                const double hk = (live && r > k) ? cb[r] : 0.0; // H(r, k)
-                const double lr = hk * isq;                     // L(r, k)
-                const double tk = cb[RW] * isq;                 // t_k
-                gv = (r == k) ? tk : ((r > k) ? gv - lr * tk : gv);
-                if (h == e && live && r >= k) Lc[wg_lcol<NF>(k) + r - k] = (r == k) ? piv * isq : lr;
-                if (tid == 0) rinv[k] = isq;
-                const double fr = hk * (isq * isq);             // L(r,k) / L(k,k)
-                if (e == 0) {
-                    // slot j = column 2(m + j) + h
-                    const double *src = cb + 2 * m + h;
-#pragma unroll
-                    for (int j = 0; j < NH; ++j) {
-                        hr[j] -= fr * src[2 * j];
-                        if ((j & 7) == 7) step_fence();  // bound the loads in flight
-                    }
-                } else {
-                    // the update of column 2(m + j + 1) + h lands in slot j: both slots 0 done
-                    const double *src = cb + 2 * (m + 1) + h;
-#pragma unroll
-                    for (int j = 0; j < NH - 1; ++j) {
-                        hr[j] = hr[j + 1] - fr * src[2 * j];
-                        if ((j & 7) == 7) step_fence();
-                    }
-                    hr[NH - 1] = 0.0;
+            for (int j = 0; j < NH; ++j) {
+                const int c = 2 * j + h;  // the callers' interleaved row layout
+                if (c <= r) {
+                    const int ti = r >> 4, tj = c >> 4, ra = r & 15, cb_ = c & 15;
+                    double *tl = F + TF::oTiles + TS * tix(ti, tj);
+                    tl[64 * (cb_ >> 2) + 16 * (cb_ & 3) + ra] = hr[j];      // stored S = H_ij'
+                    if (ti == tj && c < r) tl[64 * (ra >> 2) + 16 * (ra & 3) + cb_] = hr[j];
                 }
             }
+            if (h == 0) F[TF::oG + r] = gv;
         }
-        if (bad) status = ST_NOT_PD;
-    }
-    MPCQP_STAMP(C.stamps, 5, tst);
-    MPCQP_CUT(C.cut, 4);
-
-    if (status == ST_OK && nf > 0) {
-        // ---- J = L^-T: back substitution of L' J = I, row l published per step
+        if (tid == 0) F[TF::oFlag] = 0.0;
+        __syncthreads();
+        if (chol_inverse_mfma<NF, 2 * NWH>(F, wv)) status = ST_NOT_PD;
+        MPCQP_STAMP(C.stamps, 5, tst);
+        MPCQP_CUT(C.cut, 4);
+#pragma unroll
+        for (int j = 0; j < NH; ++j) {
+            const int c = h * NH + j;
+            Jr[j] = (live && c >= r) ? F[TF::xoff(c, r)] : 0.0;
+            if ((j & 7) == 7) step_fence();
+        }
+        double tt = 0.0;
+        if (live) {
+            for (int c = 0; c <= r; ++c) tt += F[TF::xoff(r, c)] * F[TF::oG + c];
+        }
+        gv = (live && r < nf) ? tt : 0.0;
+        __syncthreads();  // the factorisation's tiles are dead: the loop's buffers overlay them
         if (h == 0) tB[r] = (r < nf) ? gv : 0.0;
-#pragma unroll
-        for (int j = 0; j < NH; ++j) Jr[j] = (r == h * NH + j) ? 1.0 : 0.0;
-        const int lrow = live ? wg_lcol<NF>(r) - r : 0;  // L(l, r) at Lc[lrow + l], l > r
-        for (int l = nf - 1; l >= 0; --l) {
-            double *rb = colb + (l & 1) * CBW + h * NH;
-            if (r == l) {
-                const double il = rinv[l];
-#pragma unroll
-                for (int j = 0; j < NH; ++j) {
-                    Jr[j] *= il;
-                    rb[j] = Jr[j];
-                }
-            }
-            __syncthreads();
-            if (r < l) {
-                const double llr = Lc[lrow + l];
-#pragma unroll
-                for (int j = 0; j < NH; ++j) {
-                    Jr[j] -= llr * rb[j];
-                    if ((j & 7) == 7) step_fence();
-                }
-            }
-        }
+        __syncthreads();
         MPCQP_STAMP(C.stamps, 6, tst);
         MPCQP_CUT(C.cut, 5);
         // ---- unconstrained minimum x = -J t, objective -|t|^2 / 2

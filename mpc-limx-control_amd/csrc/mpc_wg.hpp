@@ -43,7 +43,7 @@ struct WgSrbmLayout {
     static constexpr int nFront = oRm + NU * NU - oU;
     // solver view (after every thread holds its H_FF half-row)
     static constexpr int oW = oU;
-    static constexpr int nSolver = WgLayout<NF>::doubles;
+    static constexpr int nSolver = WgLayout<NF>::work;
     static constexpr int nDoubles = oU + (nFront > nSolver ? nFront : nSolver);
     static constexpr size_t bytes =
         sizeof(double) * nDoubles + sizeof(int) * (NF + NV) + ((MT + 15) & ~15);
