@@ -33,6 +33,7 @@ struct FastKernels {
     size_t disc_lds = 0, cs_lds = 0, mpc_lds = 0;
     int nx = 0, nu = 0;
     int prim_nf = 0;  // free variables the one-wave kernel holds (kPairCap or its NF)
+    int nf = 0;       // NF the one-wave kernel is instantiated for
 };
 
 constexpr int kPairCap = 30;  // free variables of one half of the paired kernel (mpc_pair.hpp)
@@ -95,6 +96,7 @@ FastKernels make_fast() {
     k.mpc_lds = MpcLayout<NU, N, FRIC, NFMAX>::lds_bytes;
     k.nx = NX;
     k.nu = NU;
+    k.nf = NFMAX;
     return k;
 }
 #endif  // MPCQP_FAST_TU

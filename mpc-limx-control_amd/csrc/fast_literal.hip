@@ -6,7 +6,7 @@
 namespace mpcqp {
 
 bool pick_fast_literal(int N, int nfmax, FastKernels &k) {
-    if (N == 20 && nfmax <= 64) { k = make_fast<13, 3, 20, 1, false, 64>(); return true; }
+    if (N == 20 && nfmax <= 64) { k = make_fast<13, 3, 20, 1, false, 60>(); return true; }
     if (N == 10 && nfmax <= 32) { k = make_fast<13, 3, 10, 1, false, 32>(); return true; }
     return false;
 }

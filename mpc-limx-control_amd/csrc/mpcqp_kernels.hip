@@ -438,7 +438,7 @@ bool pick_fast(int model, int nx, int nu, int N, bool fric, int nfmax, FastKerne
     if (model == MPCQP_MODEL_LITERAL && nu == 3 && !fric) found = pick_fast_literal(N, nprim, k);
     if (found && pair_enabled()) add_fast_pair(model, N, fric, nprim, k);
     if (found) {
-        k.prim_nf = k.pair ? kPairCap : (nprim <= 32 ? 32 : 64);
+        k.prim_nf = k.pair ? kPairCap : k.nf;
         if (nfmax > k.prim_nf) add_fast_wg(model, N, fric, k);
     }
     return found;

@@ -15,7 +15,8 @@ sys.path.insert(0, os.path.join(ROOT, "mpc-limx-control_amd"))
 import numpy as np  # noqa: E402
 
 NAMES = ["setup", "Phi/xf chains", "Qe", "H_FF", "gradient", "Cholesky", "J=L^-T",
-         "unconstrained min", "dual loop", "write", "model build", "expm"]
+         "unconstrained min", "dual loop", "write", "model build", "expm",
+         "  loop: select", "  loop: project+z", "  loop: step", "  loop: update"]
 
 
 def main():
@@ -38,12 +39,13 @@ def main():
     eng.solve(d)
     eng.sync()
     assert lib().mpcqp_debug_phase_cycles(eng.ctx, buf, 16) == 0
-    cyc = np.array(buf[:12], dtype=np.float64) / args.batch
+    cyc = np.array(buf[:16], dtype=np.float64) / args.batch
     tot_cs = cyc[:10].sum()
     print(f"config {args.config}, gait {args.gait}, batch {args.batch}, mean iters "
           f"{d['iters'].float().mean().item():.2f}; cycles per QP (wave-serial)")
     for i, n in enumerate(NAMES):
-        share = cyc[i] / (tot_cs if i < 10 else cyc[10:12].sum())
+        den = tot_cs if (i < 10 or i >= 12) else cyc[10:12].sum()
+        share = cyc[i] / den if den > 0 else 0.0
         print(f"  {i:2d} {n:18s} {cyc[i]:10.0f}  {100 * share:5.1f}%")
     print(f"  condense_solve total {tot_cs:10.0f} ; discretize total {cyc[10:12].sum():10.0f}")
     eng.close()
