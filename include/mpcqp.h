@@ -42,6 +42,8 @@
  * mpcqp_batch_select_state        (new) best gait candidate per state
  * mpcqp_batch_plant_srbm          QPSolver::updateState (src/QPSolver.cpp:108-111), SRBM, batched
  * mpcqp_rollout                   the closed loop of src/qpSolver_test.cpp:38-90, batched
+ * mpcqp_set_warm_start            QPSolver::updateState -> next solveQP hot-started from the
+ *                                 previous active set (src/QPSolver.cpp:87-111), batched
  * mpcqp_fk_feet                   PinocchioKinematics::forwardKinematics + getLinkPosition
  *                                 (include/pinocchio_kinematics.h:30-43), batched
  * mpcqp_ctx_fk_feet_host          the same, host pointers (mpcQP::buildSystemModel's FK,
@@ -226,6 +228,14 @@ int mpcqp_reduce_records(mpcqp_ctx *ctx, int n, const int64_t *records, int64_t 
 int mpcqp_batch_solve_gait(mpcqp_ctx *ctx, int S, int C, const double *state, const double *feet,
                            const double *cmd, const double *phase, float swing, float stance,
                            double *U, double *cost, int *status, int *iters);
+/* Warm start of the gait solves from the previous call's active sets (the closed loop,
+ * SURVEY.md 8f row 2): on = 1 keeps each instance's final active set (bounds and friction rows
+ * in the global input numbering) and seeds the next mpcqp_batch_solve_gait / mpcqp_rollout tick
+ * with it, shifted by one horizon step; the Goldfarb-Idnani selection re-adds those constraints
+ * first.  The optimum is unchanged (the QP is strictly convex); iteration counts differ from a
+ * cold solve.  Every call resets the stored sets (the next tick starts cold).  One-wave fused
+ * kernels only (13/6/20 and the literal 13/3/20); a paired-kernel context ignores it. */
+int mpcqp_set_warm_start(mpcqp_ctx *ctx, int on);
 /* best candidate of each state (status OK, fp32 cost, lowest index; best = -1 if none):
  * best [S], best_cost [S] (nullable), Ubest [S][nu*N] (nullable).  C <= 64. */
 int mpcqp_batch_select_state(mpcqp_ctx *ctx, int S, int C, const double *cost, const int *status,

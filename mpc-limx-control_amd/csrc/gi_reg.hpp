@@ -95,12 +95,31 @@ __device__ __forceinline__ void gi_project_reg(const GiCtx &C, const double (&Jr
     if (ln >= nf) dj = 0.0;
 }
 
+// Warm start of the dual loop from the previous tick's active set (the closed-loop rollout,
+// SURVEY.md 8f row 2; QPSolver::updateState, src/QPSolver.cpp:108-111, then the next tick's
+// solveQP).  words: bit v = lower bound of input v, bit nV + v = its upper bound, bit
+// 2 nV + 4 (k nfeet + s) + t = friction row t of foot s at step k (global numbering, so the
+// set survives a change of the free-variable map).  The previous horizon shifted by one step
+// (step k here = step k + 1 there; the last step repeats) marks guessed constraints; while any
+// guessed constraint is violated the selection takes the lowest-id one of those instead of
+// the most violated one, and each is guessed only once.  The optimum is the same unique point;
+// only the order of the adds (and so the number of drops) changes.  The final active set is
+// written back over the same words.
+struct WarmSet {
+    unsigned long long *words;  // this instance's words (read at the start, written at the end)
+    int n;                      // words per instance
+};
+__device__ __forceinline__ bool warm_bit(const unsigned long long *w, int i) {
+    return (w[i >> 6] >> (i & 63)) & 1ull;
+}
+
 // h: lane p holds row p of H_FF (columns < nf meaningful), g: lane p holds g_p.
 // rowbuf: 5 NF doubles of LDS (16-byte aligned): row / column broadcast buffers, the
 // rotation pairs and 1/R(j,j).  Broadcasts go through LDS (one ds_read_b128 brings two values to every
 // lane) rather than v_readlane pairs, which cost VALU issue slots.  Fills C.{status,x,u,fval,act,q,iters}.
 template <int NF>
-__device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, double *rowbuf) {
+__device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, double *rowbuf,
+                                           const WarmSet *warm = nullptr) {
     static_assert(NF <= kWave, "register path holds at most 64 free variables");
     GiLds &L = C.L;
     const SolveProblem &P = *C.P;
@@ -257,6 +276,21 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         if (c % 3 == 2 && ((P.contact >> (2 * k + sft)) & 1ull))
             fbase = 2 * nf + 4 * (k * P.nfeet + sft);
     }
+    int gmask = 0;  // guessed constraints of this lane: bit 0 lower, 1 upper, 2 + t friction row t
+    if (warm && status == ST_OK && ln < nf) {
+        const unsigned long long *w = warm->words;
+        const int v = L.fid[ln], k = v / P.nu, c = v % P.nu;
+        const int ks = k + 1 < P.N ? k + 1 : k;
+        const int vs = ks * P.nu + c;
+        if (warm_bit(w, vs)) gmask |= 1;
+        if (warm_bit(w, P.nV + vs)) gmask |= 2;
+        if (fbase >= 0) {
+            const int fb = 2 * P.nV + 4 * (ks * P.nfeet + c / 3);
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                if (warm_bit(w, fb + t)) gmask |= 4 << t;
+        }
+    }
     while (!done) {
         if (fresh) {
             // ---- step 1: most violated inactive constraint (lowest id on ties)
@@ -267,11 +301,15 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                 const double b0 = L.cb[ln], b1 = L.cb[ln + nf];
                 if (s0 == 1) {
                     const double sl_ = x - b0;
-                    if (sl_ < -kFeasTol * (1.0 + fabs(b0))) { best = sl_; bid = ln; }
+                    if (sl_ < -kFeasTol * (1.0 + fabs(b0))) {
+                        best = (gmask & 1) ? -INFINITY : sl_;
+                        bid = ln;
+                    }
                 }
                 if (s1 == 1) {
                     const double sl_ = -x - b1;
-                    if (sl_ < -kFeasTol * (1.0 + fabs(b1)) && sl_ < best) { best = sl_; bid = ln + nf; }
+                    const double kv = (gmask & 2) ? -INFINITY : sl_;
+                    if (sl_ < -kFeasTol * (1.0 + fabs(b1)) && kv < best) { best = kv; bid = ln + nf; }
                 }
             }
             if (C.nfric > 0) {
@@ -285,7 +323,8 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                         s += P.mu * x;
                         s += sg * ((t >> 1) ? xm1 : xm2);
                         const double sl_ = s - 0.0;
-                        if (sl_ < -kFeasTol * (1.0 + fabs(0.0)) && sl_ < best) { best = sl_; bid = fbase + t; }
+                        const double kv = (gmask & (4 << t)) ? -INFINITY : sl_;
+                        if (sl_ < -kFeasTol * (1.0 + fabs(0.0)) && kv < best) { best = kv; bid = fbase + t; }
                     }
                 }
             }
@@ -294,6 +333,11 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             p = bid;
             if (ln == q) u = 0.0;
             fresh = false;
+            if (gmask) {  // a guess is used once
+                if (p < nf) { if (ln == p) gmask &= ~1; }
+                else if (p < 2 * nf) { if (ln == p - nf) gmask &= ~2; }
+                else if (fbase >= 0 && p >= fbase && p < fbase + 4) gmask &= ~(4 << (p - fbase));
+            }
         }
         double dj, sp;
         gi_project_reg<NF>(C, Jr, p, x, dj, sp, rowbuf);
@@ -462,6 +506,26 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         wave_sync();
     }
     MPCQP_STAMP(C.stamps, 8, tst); MPCQP_CUT(C.cut, 7);
+    if (warm) {
+        // this tick's active set, in the global numbering, for the next tick
+        unsigned long long *wl = reinterpret_cast<unsigned long long *>(rowbuf);
+        wave_sync();
+        if (ln < warm->n) wl[ln] = 0ull;
+        wave_sync();
+        if (status == ST_OK && ln < nf) {
+            const int v = L.fid[ln], k = v / P.nu, c = v % P.nu;
+            if (L.st[ln] == 2) atomicOr(&wl[v >> 6], 1ull << (v & 63));
+            if (L.st[ln + nf] == 2) atomicOr(&wl[(P.nV + v) >> 6], 1ull << ((P.nV + v) & 63));
+            if (fbase >= 0) {
+                const int fb = 2 * P.nV + 4 * (k * P.nfeet + c / 3);
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    if (L.st[fbase + t] == 2) atomicOr(&wl[(fb + t) >> 6], 1ull << ((fb + t) & 63));
+            }
+        }
+        wave_sync();
+        if (ln < warm->n) warm->words[ln] = wl[ln];
+    }
     C.status = status;
     C.x = x;
     C.u = u;

@@ -51,6 +51,8 @@ struct MpcArgs {
     int cands;
     float swing, stance;  // MPCParam::swing_time / stance_time (float, include/MPCParam.h:48-49)
     int *ovf;  // overflow list (mpc_wg.hpp) for instances beyond the kernel's free capacity
+    unsigned long long *warm;  // GEN one-wave kernels: per-instance active-set words (WarmSet)
+    int warm_words;
 };
 
 // overflow list layout (int): [0] count, [1] unused, [2 ..] instance ids
@@ -475,7 +477,12 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
         wave_sync();
         MPCQP_STAMP(a.stamps, 3, tst);
         MPCQP_CUT(a.cut, 3);
-        gi_run_reg<NF>(C, h, gp, D + Lay::oRow);
+        if (GEN && a.warm) {
+            WarmSet ws{a.warm + (size_t)b * a.warm_words, a.warm_words};
+            gi_run_reg<NF>(C, h, gp, D + Lay::oRow, &ws);
+        } else {
+            gi_run_reg<NF>(C, h, gp, D + Lay::oRow);
+        }
     }
 #ifdef MPCQP_CUTS
     if (a.cut >= 4 && a.cut <= 7) return;

@@ -536,6 +536,9 @@ struct mpcqp_ctx {
     size_t rbuf_cap = 0;
     void *fkbuf = nullptr;  // mpcqp_ctx_fk_feet_host staging
     size_t fkbuf_cap = 0;
+    void *dwarm = nullptr;  // warm start: per-instance active-set words (gi_reg.hpp WarmSet)
+    size_t warm_cap = 0;
+    int warm_on = 0, warm_fresh = 0;
 };
 
 extern "C" {
@@ -884,6 +887,7 @@ int mpcqp_ctx_destroy(mpcqp_ctx *c) {
     hipFree(c->hbuf);
     hipFree(c->rbuf);
     hipFree(c->fkbuf);
+    hipFree(c->dwarm);
     hipFree(c->scratchH);
     hipFree(c->scratchF);
     if (c->ev_ok)
@@ -1025,6 +1029,25 @@ static size_t host_stage_bytes(const mpcqp_ctx *c, size_t B) {
 static size_t rollout_bytes(const mpcqp_ctx *c, size_t S, size_t C) {
     const size_t B = S * C, nV = (size_t)c->m.nu * c->m.N;
     return sizeof(double) * (B * nV + B + S * nV + S) + sizeof(int) * (2 * B + S) + 64;
+}
+
+static int warm_words(const mpcqp_ctx *c) {
+    return (2 * c->m.nu * c->m.N + 8 * c->m.N + 63) / 64;
+}
+
+// the warm-start words of B instances, zeroed (cold) after mpcqp_set_warm_start or a resize
+static int ensure_warm(mpcqp_ctx *c, int B) {
+    const size_t bytes = sizeof(unsigned long long) * warm_words(c) * (size_t)B;
+    if (c->warm_cap < bytes) {
+        int rc = ensure_bytes(c, &c->dwarm, &c->warm_cap, bytes);
+        if (rc) return rc;
+        c->warm_fresh = 1;
+    }
+    if (c->warm_fresh) {
+        if (hipMemsetAsync(c->dwarm, 0, c->warm_cap, c->stream) != hipSuccess) return MPCQP_ERR_DEVICE;
+        c->warm_fresh = 0;
+    }
+    return MPCQP_OK;
 }
 
 // overflow list for B instances (grown on demand; mpcqp_ctx_reserve sizes it up front)
@@ -1256,6 +1279,7 @@ int mpcqp_ctx_reserve(mpcqp_ctx *c, int B) {
     if (!rc && c->fast && c->fk.wg) rc = ensure_list(c, B);
     if (!rc && c->fast && c->fk.mpc_gen)
         rc = ensure_bytes(c, &c->rbuf, &c->rbuf_cap, rollout_bytes(c, B, 1));
+    if (!rc && c->warm_on && c->fast && c->fk.mpc_gen && !c->fk.pair_gen) rc = ensure_warm(c, B);
     if (!rc && !c->fast) rc = ensure_bytes(c, (void **)&c->dAB, &c->ab_cap, sizeof(double) * ab * B);
     if (!rc && !c->fast) rc = ensure_scratch_hf(c, B);
     if (!rc) rc = hip_status(hipStreamSynchronize(c->stream));
@@ -1314,6 +1338,13 @@ int mpcqp_batch_solve_host(mpcqp_ctx *c, int B, const double *x0, const double *
     return hip_status(hipStreamSynchronize(c->stream));
 }
 
+int mpcqp_set_warm_start(mpcqp_ctx *c, int on) {
+    if (!c) return MPCQP_ERR_BAD_ARG;
+    c->warm_on = on ? 1 : 0;
+    c->warm_fresh = 1;  // the next gait solve starts cold
+    return MPCQP_OK;
+}
+
 int mpcqp_batch_solve_gait(mpcqp_ctx *c, int S, int C, const double *state, const double *feet,
                            const double *cmd, const double *phase, float swing, float stance,
                            double *U, double *cost, int *status, int *iters) {
@@ -1338,6 +1369,12 @@ int mpcqp_batch_solve_gait(mpcqp_ctx *c, int S, int C, const double *state, cons
     a.cost = cost;
     a.status = status;
     a.iters = iters;
+    if (c->warm_on && !c->fk.pair_gen) {  // the one-wave kernels (N = 20 / literal) take it
+        const int rw = ensure_warm(c, B);
+        if (rw) return rw;
+        a.warm = reinterpret_cast<unsigned long long *>(c->dwarm);
+        a.warm_words = warm_words(c);
+    }
     tbegin(c, 1);
     const int rc = launch_mpc(c, true, B, &a);
     tend(c, 1);

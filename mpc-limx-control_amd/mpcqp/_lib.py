@@ -30,7 +30,7 @@ EXPORTS = [
     "mpcqp_enable_timing", "mpcqp_last_kernel_ms",
     "mpcqp_batch_solve_gait", "mpcqp_batch_select_state", "mpcqp_batch_plant_srbm",
     "mpcqp_rollout", "mpcqp_fk_feet", "mpcqp_kf_update", "mpcqp_ctx_reserve",
-    "mpcqp_ctx_fk_feet_host",
+    "mpcqp_ctx_fk_feet_host", "mpcqp_set_warm_start",
     "mpcqp_status_string", "mpcqp_device_count",
 ]
 
@@ -92,6 +92,7 @@ def lib():
     L.mpcqp_fk_feet.argtypes = [vp, i, vp, vp, i, vp]
     L.mpcqp_ctx_fk_feet_host.argtypes = [vp, i, vp, vp, i, vp]
     L.mpcqp_ctx_reserve.argtypes = [vp, i]
+    L.mpcqp_set_warm_start.argtypes = [vp, i]
     L.mpcqp_kf_update.argtypes = [vp, i, d] + [vp] * 7
     L.mpcqp_enable_timing.argtypes = [vp, i]
     L.mpcqp_last_kernel_ms.argtypes = [vp, i]

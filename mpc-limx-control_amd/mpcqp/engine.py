@@ -65,6 +65,10 @@ class BatchEngine:
         self.reserve(B)
         return out
 
+    def set_warm_start(self, on: bool = True):
+        """seed each gait solve with the previous tick's active sets (mpcqp_set_warm_start)"""
+        check("mpcqp_set_warm_start", lib().mpcqp_set_warm_start(self.ctx, int(bool(on))))
+
     def reserve(self, B: int):
         """size the context's scratch for B instances: no allocation on the solve path"""
         check("mpcqp_ctx_reserve", lib().mpcqp_ctx_reserve(self.ctx, int(B)))

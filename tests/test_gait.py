@@ -152,3 +152,53 @@ def test_rollout_ticks_rederived_by_oracle(gpu, orc):
         state = traj[k].copy()
         phase = phase + p["Ts"]
     eng.close()
+
+
+def _closed_loop_iters(p, g, K, warm, orc=None):
+    """K ticks of solve_gait -> select_state -> plant on one context (the mpcqp_rollout loop),
+    optionally warm-started; every tick's U / cost re-derived by the oracle when orc is given.
+    Returns the per-tick iteration totals."""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    eng = BatchEngine(p)
+    eng.set_warm_start(warm)
+    dg = eng.upload_gait(g)
+    totals = []
+    for k in range(K):
+        if orc is not None:
+            gi = mpcqp.gait_inputs(p, dict(state=dg["state"].cpu().numpy(),
+                                           feet=dg["feet"].cpu().numpy(), cmd=g["cmd"],
+                                           phase=dg["phase"].cpu().numpy()))
+        eng.solve_gait(dg)
+        eng.select_state(dg)
+        eng.sync()
+        it = dg["iters"].cpu().numpy()
+        totals.append(int(it.sum()))
+        if orc is not None:
+            ref = orc.srbm_batch(p, gi["x0"], gi["xref"], gi["lin"], gi["contact"])
+            st = dg["status"].cpu().numpy()
+            np.testing.assert_array_equal(st, ref["status"])
+            U = dg["U"].cpu().numpy()
+            err = np.abs(U - ref["U"]).max(axis=1) / np.maximum(1.0, np.abs(ref["U"]).max(axis=1))
+            assert err.max() <= 1e-8, (k, err.max())
+            np.testing.assert_allclose(dg["cost"].cpu().numpy(), ref["cost"], rtol=1e-9, atol=1e-9)
+        eng.plant(dg)
+    eng.sync()
+    eng.close()
+    return np.array(totals)
+
+
+@pytest.mark.gpu
+def test_rollout_warm_start_matches_oracle_and_saves_passes(gpu, orc):
+    """Warm start of the closed loop (mpcqp_set_warm_start) at config C:
+    every tick's plans equal the oracle's cold solve of the same inputs (unique optimum), the
+    first tick is cold (identical iteration count), and the warm ticks take fewer dual passes
+    than the cold loop over the same ticks (tools/warm_start_ab.py: up to 53 % fewer)."""
+    import mpcqp
+    p = mpcqp.model_params("C")
+    S, Cc, K = 32, 8, 8
+    g = mpcqp.make_gait_states(p, S, seed=9, candidates=Cc)
+    warm = _closed_loop_iters(p, g, K, True, orc)
+    cold = _closed_loop_iters(p, g, K, False)
+    assert warm[0] == cold[0]
+    assert warm[1:].sum() < 0.9 * cold[1:].sum(), (warm, cold)
