@@ -282,7 +282,11 @@ __device__ __forceinline__ void expm_pade_solve(int nx, int ns, const double *U,
         X[e] = (e / nx >= nx) ? n - d : n;
     }
     wave_sync();
-    // LU with partial pivoting on D[:, 0:nx], applied to all ns columns of X
+    // LU with partial pivoting on D[:, 0:nx], applied to all ns columns of X.  Lane jj owns
+    // one column of [D(:, k+1:) | X] per step and updates it in registers: every load of a
+    // step is issued before its stores (LDS pointers may alias, so a load-after-store chain
+    // would cost a round trip per element).  nx <= 32 (MPCQP_MAX_NX), nx + ns <= 64.
+    constexpr int MX = 32;
     for (int k = 0; k < nx; ++k) {
         double pv = -1.0;
         int pi = 0x7fffffff;
@@ -301,29 +305,50 @@ __device__ __forceinline__ void expm_pade_solve(int nx, int ns, const double *U,
             wave_sync();
         }
         const double piv = D[k * nx + k];
-        const int rows = nx - k - 1;
+        // multipliers l_i = D(i, k) / piv, one division per row, kept in place (column k below
+        // the pivot is not read again: the back substitution reads the upper factor only)
+        for (int i = k + 1 + lane(); i < nx; i += kWave) D[k * nx + i] = D[k * nx + i] / piv;
+        wave_sync();
         // update D(i, j) for j > k and X(i, j) for all j, i > k
         const int wD = nx - k - 1, wtot = wD + ns;
-        for (int e = lane(); e < rows * wtot; e += kWave) {
-            const int i = k + 1 + e % rows, jj = e / rows;
-            const double l = D[k * nx + i] / piv;
-            if (jj < wD) {
-                const int j = k + 1 + jj;
-                D[j * nx + i] -= l * D[j * nx + k];
-            } else {
-                const int j = jj - wD;
-                X[j * nx + i] -= l * X[j * nx + k];
+        const int jj = lane();
+        if (jj < wtot) {
+            double *col = jj < wD ? D + (k + 1 + jj) * nx : X + (jj - wD) * nx;
+            double lm[MX], v[MX];
+#pragma unroll
+            for (int i = 0; i < MX; ++i) {
+                const bool in = i > k && i < nx;
+                lm[i] = in ? D[k * nx + i] : 0.0;
+                v[i] = in ? col[i] : 0.0;
             }
+            const double ck = col[k];
+#pragma unroll
+            for (int i = 0; i < MX; ++i)
+                if (i > k && i < nx) col[i] = v[i] - lm[i] * ck;
         }
         wave_sync();
     }
-    // back substitution (each lane owns a column of X)
-    for (int j = lane(); j < ns; j += kWave)
-        for (int i = nx - 1; i >= 0; --i) {
-            double s = X[j * nx + i];
-            for (int l = i + 1; l < nx; ++l) s -= D[l * nx + i] * X[j * nx + l];
-            X[j * nx + i] = s / D[i * nx + i];
+    // back substitution, lane j owns column j of X (in registers)
+    {
+        const int j = lane();
+        if (j < ns) {
+            double v[MX];
+#pragma unroll
+            for (int i = 0; i < MX; ++i) v[i] = i < nx ? X[j * nx + i] : 0.0;
+#pragma unroll
+            for (int i = MX - 1; i >= 0; --i) {
+                if (i >= nx) continue;
+                double s = v[i];
+#pragma unroll
+                for (int l = i + 1; l < MX; ++l)
+                    if (l < nx) s -= D[l * nx + i] * v[l];
+                v[i] = s / D[i * nx + i];
+            }
+#pragma unroll
+            for (int i = 0; i < MX; ++i)
+                if (i < nx) X[j * nx + i] = v[i];
         }
+    }
     wave_sync();
 }
 

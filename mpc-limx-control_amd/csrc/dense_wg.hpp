@@ -121,7 +121,7 @@ __device__ __forceinline__ void dense_mpc_one(const MpcArgs &a, int b, unsigned 
     }
     __syncthreads();
     // ---- discretisation (the workgroup, matrix cores) and the free map / bounds (wave 0)
-    wg_expm(NX, NS, D + Lay::oT, D + Lay::oWs, AB, tid, NT, wv, NT / 64);
+    wg_expm(NX, NS, D + Lay::oT, D + Lay::oWs, AB, tid, NT, wv, NT / 64, a.stamps);
     if (wv == 0) {
         gi_setup(C);
         if (C.nf > a.max_free) C.status = ST_BAD_DIMS;

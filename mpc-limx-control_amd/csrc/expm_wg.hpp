@@ -58,7 +58,9 @@ __device__ __forceinline__ void wg_alg_comb(int nx, int ns, double *out, const d
 // wave_expm by the workgroup (nt threads, nw waves).  T (nx x ns, scaled by Ts) is overwritten
 // when scaling; ws: 7 nx ns doubles; E: the result top block.  Every thread must call it.
 __device__ __forceinline__ void wg_expm(int nx, int ns, double *T, double *ws, double *E, int tid,
-                                        int nt, int wv, int nw) {
+                                        int nt, int wv, int nw,
+                                        unsigned long long *stamps = nullptr) {
+    MPCQP_STAMP_INIT(tx);
     const int sz = nx * ns;
     double *A2 = ws, *A4 = ws + sz, *A6 = ws + 2 * sz, *A8 = ws + 3 * sz, *U = ws + 4 * sz,
            *V = ws + 5 * sz, *W = ws + 6 * sz;
@@ -128,13 +130,17 @@ __device__ __forceinline__ void wg_expm(int nx, int ns, double *T, double *ws, d
         for (int e = tid; e < sz; e += nt) V[e] += A8[e];
         __syncthreads();
     }
+    MPCQP_STAMP(stamps, 12, tx);
     if (wv == 0) expm_pade_solve(nx, ns, U, V, A2, E);
     __syncthreads();
+    MPCQP_STAMP(stamps, 13, tx);
     for (int s = 0; s < squarings; ++s) {
         wg_alg_mul(nx, ns, E, E, 1.0, W, wv, nw);
         for (int e = tid; e < sz; e += nt) E[e] = W[e];
         __syncthreads();
     }
+    MPCQP_STAMP(stamps, 14, tx);
+    (void)stamps;
 }
 
 }  // namespace mpcqp

@@ -16,7 +16,7 @@ import numpy as np  # noqa: E402
 
 NAMES = ["setup", "Phi/xf chains", "Qe", "H_FF", "gradient", "Cholesky", "J=L^-T",
          "unconstrained min", "dual loop", "write", "model build", "expm",
-         "  loop: select", "  loop: project+z", "  loop: step", "  loop: update"]
+         "  sub 12", "  sub 13", "  sub 14", "  sub 15"]
 
 
 def main():
