@@ -17,6 +17,7 @@
 // index is a compile-time constant (no scratch), and cross-lane reads are v_readlane with
 // constant lane indices.
 #pragma once
+#include "chol_reg.hpp"
 #include "gi_solver.hpp"
 
 namespace mpcqp {
@@ -117,7 +118,9 @@ __device__ __forceinline__ bool warm_bit(const unsigned long long *w, int i) {
 // rowbuf: 5 NF doubles of LDS (16-byte aligned): row / column broadcast buffers, the
 // rotation pairs and 1/R(j,j).  Broadcasts go through LDS (one ds_read_b128 brings two values to every
 // lane) rather than v_readlane pairs, which cost VALU issue slots.  Fills C.{status,x,u,fval,act,q,iters}.
-template <int NF>
+// TILES: the start comes from the packed H_FF in L.R (Hb) through the blocked MFMA
+// factorisation of chol_reg.hpp instead of the column sweeps over h (h unused).
+template <int NF, bool TILES = false>
 __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, double *rowbuf,
                                            const WarmSet *warm = nullptr) {
     static_assert(NF <= kWave, "register path holds at most 64 free variables");
@@ -134,7 +137,19 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
     double *Lc = L.R;  // column-packed L (the R space is free until the dual loop)
     MPCQP_STAMP_INIT(tst);
 
-    if (status == ST_OK && nf > 0) {
+    if constexpr (TILES) {
+        if (status == ST_OK && nf > 0) {
+            bool bad = false;
+            double tt = 0.0;
+            reg_chol_inverse_mfma<NF>(L.R, nf, g, L.R, Jr, tt, bad);
+            if (bad) status = ST_NOT_PD;
+            gv = (ln < NF) ? tt : 0.0;
+            if (ln < NF) colb[ln] = gv;
+            wave_sync();
+        }
+        MPCQP_STAMP(C.stamps, 5, tst); MPCQP_CUT(C.cut, 4);
+    }
+    if (!TILES && status == ST_OK && nf > 0) {
         // ---- Cholesky, right-looking; lane i owns row i.  h is padded with the identity
         //      beyond nf (and g with 0), so every step runs unpredicated (upper-triangle junk
         //      is never read).  The forward solve L t = g runs in the same sweep.
@@ -202,8 +217,9 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         }
         if (bad) status = ST_NOT_PD;
     }
-    MPCQP_STAMP(C.stamps, 5, tst); MPCQP_CUT(C.cut, 4);
+    if constexpr (!TILES) { MPCQP_STAMP(C.stamps, 5, tst); MPCQP_CUT(C.cut, 4); }
     if (status == ST_OK && nf > 0) {
+      if constexpr (!TILES) {
         // ---- columns of L^-1, right-looking: lane c solves L y = e_c (lane 63: L t = g when
         //      NF < 64) column by column of L, whose entries are uniform-address LDS
         //      broadcasts; a step's updates are independent FMAs.  y = column c of L^-1 =
@@ -243,6 +259,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         }
         wave_sync();
         if constexpr (T63) gv = (ln < NF) ? colb[ln] : 0.0;
+      }
         double s4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int j = 0; j < NF; ++j) {

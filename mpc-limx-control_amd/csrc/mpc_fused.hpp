@@ -27,6 +27,14 @@
 
 namespace mpcqp {
 
+// one-QP kernels above 32 free variables start the solver with the blocked MFMA
+// factorisation (chol_reg.hpp); MPCQP_REG_TILES=0 keeps the column sweeps (A/B builds)
+#ifndef MPCQP_REG_TILES
+#define MPCQP_REG_TILES 1
+#endif
+template <int NF>
+constexpr bool kRegTiles = MPCQP_REG_TILES && NF > 32;
+
 struct MpcArgs {
     int B;
     double Ts, mass;
@@ -469,19 +477,21 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
         }
         wave_sync();
         double h[NF];
+        if constexpr (!kRegTiles<NF>) {
 #pragma unroll
-        for (int q = 0; q < NF; ++q) {
-            const bool in = ok && ln < nf && q < nf && q <= ln;
-            h[q] = in ? Hb[lrow(ln) + q] : ((q == ln) ? 1.0 : 0.0);
+            for (int q = 0; q < NF; ++q) {
+                const bool in = ok && ln < nf && q < nf && q <= ln;
+                h[q] = in ? Hb[lrow(ln) + q] : ((q == ln) ? 1.0 : 0.0);
+            }
+            wave_sync();
         }
-        wave_sync();
         MPCQP_STAMP(a.stamps, 3, tst);
         MPCQP_CUT(a.cut, 3);
         if (GEN && a.warm) {
             WarmSet ws{a.warm + (size_t)b * a.warm_words, a.warm_words};
-            gi_run_reg<NF>(C, h, gp, D + Lay::oRow, &ws);
+            gi_run_reg<NF, kRegTiles<NF>>(C, h, gp, D + Lay::oRow, &ws);
         } else {
-            gi_run_reg<NF>(C, h, gp, D + Lay::oRow);
+            gi_run_reg<NF, kRegTiles<NF>>(C, h, gp, D + Lay::oRow);
         }
     }
 #ifdef MPCQP_CUTS

@@ -415,8 +415,10 @@ def test_pair_kernel_matches_single_and_oracle(gpu, orc, monkeypatch):
     np.testing.assert_array_equal(pair["status"], single["status"])
     assert np.all(pair["status"][bad_dims] == 1) and np.all(pair["status"][~bad_dims] == 0)
     np.testing.assert_array_equal(pair["iters"], single["iters"])
-    np.testing.assert_allclose(pair["U"], single["U"], rtol=0, atol=1e-12)
-    np.testing.assert_allclose(pair["cost"], single["cost"], rtol=1e-12, atol=1e-12)
+    # blocked MFMA factorisation in the one-QP kernel vs column sweeps in the paired one
+    sc = np.maximum(1.0, np.abs(single["U"]).max(axis=1, keepdims=True))
+    assert np.all(np.abs(pair["U"] - single["U"]) <= 1e-10 * sc)
+    np.testing.assert_allclose(pair["cost"], single["cost"], rtol=1e-10, atol=1e-10)
     ok = ~bad_dims
     ref = orc.srbm_batch(p, batch["x0"][ok], batch["xref"][ok], batch["lin"][ok], ct[ok])
     assert np.all(ref["status"] == 0)
@@ -430,7 +432,9 @@ def test_pair_kernel_matches_single_and_oracle(gpu, orc, monkeypatch):
 def test_pair_kernel_full_size_vs_single(gpu, monkeypatch):
     """metric batch (65536): the paired kernel's schedule-sorted instance assignment writes
     every instance exactly once (outputs pre-filled with sentinels) and agrees with the
-    one-QP kernel everywhere: status and iteration counts equal, U / cost to 1e-12."""
+    one-QP kernel everywhere: status and iteration counts equal, U / cost to 1e-10 relative
+    (the one-QP kernel factors H_FF with the blocked MFMA algorithm of chol_reg.hpp, the
+    paired kernel column by column: same operations, different summation order)."""
     import torch
     import mpcqp
     from mpcqp.engine import BatchEngine
@@ -459,8 +463,9 @@ def test_pair_kernel_full_size_vs_single(gpu, monkeypatch):
     assert np.all(a["status"] == 0) and np.all(b["status"] == 0)
     assert np.all(np.isfinite(a["U"])) and np.all(np.isfinite(a["cost"]))
     np.testing.assert_array_equal(a["iters"], b["iters"])
-    np.testing.assert_allclose(a["U"], b["U"], rtol=0, atol=1e-12)
-    np.testing.assert_allclose(a["cost"], b["cost"], rtol=1e-12, atol=1e-12)
+    scale = np.maximum(1.0, np.abs(b["U"]).max(axis=1, keepdims=True))
+    assert np.all(np.abs(a["U"] - b["U"]) <= 1e-10 * scale)
+    np.testing.assert_allclose(a["cost"], b["cost"], rtol=1e-10, atol=1e-10)
 
 
 def test_pair_kernel_literal_model(gpu, orc, monkeypatch):
@@ -475,7 +480,8 @@ def test_pair_kernel_literal_model(gpu, orc, monkeypatch):
     pair = run_batch(p, batch)
     np.testing.assert_array_equal(pair["status"], single["status"])
     np.testing.assert_array_equal(pair["iters"], single["iters"])
-    np.testing.assert_allclose(pair["U"], single["U"], rtol=0, atol=1e-12)
+    sc = np.maximum(1.0, np.abs(single["U"]).max(axis=1, keepdims=True))
+    assert np.all(np.abs(pair["U"] - single["U"]) <= 1e-10 * sc)
     ref = orc.srbm_batch(p, batch["x0"], batch["xref"], batch["lin"], batch["contact"])
     for i in range(B):
         assert u_close(pair["U"][i], ref["U"][i]), i
