@@ -250,6 +250,15 @@ def time_config(config, B, seed, steps=10, warmup=2, gait=None, device=0):
                max_solver_iters=int(it.max()), solved_frac=float(np.mean(st == 0)),
                algorithmic_flops_per_qp=f_qp, achieved_tflops=ach,
                frac=ach / FP64_PEAK_TFLOPS)
+    ex = _profile_json(f"pmc_flops_{config}.json")
+    if ex and ex.get("batch") == B and gait is None:
+        # executed FP64 work of this kernel (64 lanes x SQ_INSTS_VALU_FLOPS_FP64 + 512 x MFMA
+        # ops, an upper bound) from the committed PMC pass, over this run's kernel time
+        out["executed_tflops"] = ex["executed_flops_per_launch"] / (ms * 1e-3) / 1e12
+        out["pipe_frac"] = out["executed_tflops"] / FP64_PEAK_TFLOPS
+        out["mfma_tflops"] = ex["mfma_flops_per_launch"] / (ms * 1e-3) / 1e12
+        out["mfma_busy_frac"] = ex.get("mfma_busy_frac")
+        out["pmc_source"] = f"profiles/pmc_flops_{config}.json ({ex.get('tag')})"
     eng.close()
     return out
 
