@@ -365,7 +365,8 @@ def main():
         Bl = batch_local["x0"].shape[0] if not dry else batch_local["B"]
         rec = torch.zeros(1 + nV, dtype=torch.int64, device=dev)
         gathered = torch.zeros((world, 1 + nV), dtype=torch.int64, device=dev)
-        best = torch.zeros(1 + nV, dtype=torch.int64, device=dev)
+        # one rank: the record k_select_min writes IS the selection (no copy launch per step)
+        best = torch.zeros(1 + nV, dtype=torch.int64, device=dev) if world > 1 else rec
         if dry:
             cost, status, U = batch_local["cost"], batch_local["status"], batch_local["U"]
             eng = None
@@ -374,8 +375,7 @@ def main():
                 rec.copy_(torch.from_numpy(host_record(cost, status, U, index_base)))
                 if world > 1:
                     select_global(dist, rec, gathered, best, host_reduce_records)
-                else:
-                    best.copy_(rec)
+                # world == 1: best is rec
         else:
             from mpcqp.engine import BatchEngine
             eng = BatchEngine(p, device=local)
@@ -386,8 +386,7 @@ def main():
                 eng.select_record(d, rec, index_base=index_base)
                 if world > 1:
                     select_global(dist, rec, gathered, best, eng.reduce_records)
-                else:
-                    best.copy_(rec)
+                # world == 1: best is rec
 
         def sync():
             if not dry:
@@ -417,8 +416,7 @@ def main():
             e[3].record(stream)
             if world > 1:
                 select_global(dist, rec, gathered, best, eng.reduce_records)
-            else:
-                best.copy_(rec)
+            # world == 1: best is rec
         sync()
         if world > 1:
             dist.barrier()
