@@ -82,6 +82,11 @@ struct GiLds {
     int ld;
 };
 
+// value of a fixed input (xfull == nullptr: the fused one-QP kernels, whose fixed inputs are 0)
+__device__ __forceinline__ double xfixed(const GiLds &L, int v) {
+    return L.xfull ? L.xfull[v] : 0.0;
+}
+
 __device__ __forceinline__ GiLds gi_carve(unsigned char *base, int nfmax, int nV, int mA) {
     GiLds L;
     L.ld = nfmax | 1;
@@ -151,8 +156,8 @@ __device__ __forceinline__ double gi_cons_b(const GiCtx &C, int id) {
         const int vz = k * P.nu + 3 * sft + 2, vt = k * P.nu + 3 * sft + (t >> 1);
         const double sg = (t & 1) ? 1.0 : -1.0;
         double b = 0.0;
-        if (L.pos[vz] < 0) b -= P.mu * L.xfull[vz];
-        if (L.pos[vt] < 0) b -= sg * L.xfull[vt];
+        if (L.pos[vz] < 0) b -= P.mu * xfixed(L, vz);
+        if (L.pos[vt] < 0) b -= sg * xfixed(L, vt);
         return b;
     }
     const int r = id - 2 * nf - nfric, row = r >> 1, side = r & 1;
@@ -256,7 +261,7 @@ __device__ __forceinline__ void gi_setup(GiCtx &C) {
         const int before = __popcll(m & ((1ull << ln) - 1ull));
         if (valid) {
             L.pos[v] = freev ? nf + before : -1;
-            L.xfull[v] = freev ? 0.0 : lo;
+            if (L.xfull) L.xfull[v] = freev ? 0.0 : lo;
             if (freev && nf + before < nfmax) L.fid[nf + before] = v;
         }
         nf += __popcll(m);
@@ -282,7 +287,7 @@ __device__ __forceinline__ void gi_setup(GiCtx &C) {
                 const double sg = (t & 1) ? 1.0 : -1.0;
                 if (L.pos[vz] >= 0 || L.pos[vt] >= 0) s = 1;
                 else {
-                    const double bb = -(P.mu * L.xfull[vz] + sg * L.xfull[vt]);
+                    const double bb = -(P.mu * xfixed(L, vz) + sg * xfixed(L, vt));
                     if (bb > kFeasTol * (1.0 + fabs(bb))) s = 4;  // 0 >= b violated
                 }
             }
@@ -294,7 +299,7 @@ __device__ __forceinline__ void gi_setup(GiCtx &C) {
             for (int v = 0; v < nV; ++v) {
                 const double a = rowA(P, row, v);
                 if (L.pos[v] >= 0) anyfree |= (a != 0.0);
-                else fix += a * L.xfull[v];
+                else fix += a * xfixed(L, v);
             }
             if (side == 0) L.rowfix[row] = fix;
             if (lo > hi) s = 4;
@@ -582,7 +587,7 @@ __device__ __forceinline__ void gi_write(GiCtx &C, const SolveOut &O) {
     const bool have_map = nf <= C.nfmax && nf <= kWave;
     for (int v = ln; v < nV; v += kWave) {
         const int pv = L.pos[v];
-        if (pv < 0 || !have_map) O.x[v] = (pv < 0) ? L.xfull[v] : 0.0;
+        if (pv < 0 || !have_map) O.x[v] = (pv < 0) ? xfixed(L, v) : 0.0;
     }
     if (have_map && ln < nf) O.x[L.fid[ln]] = C.x;
     if (ln == 0) {
@@ -593,7 +598,7 @@ __device__ __forceinline__ void gi_write(GiCtx &C, const SolveOut &O) {
     if (O.y) {
         // multipliers: y_b (nV) then y_A (mA) with H x + f = y_b + A' y_A, built in LDS
         for (int v = ln; v < nV + mA; v += kWave) L.ys[v] = 0.0;
-        if (have_map && ln < nf) L.xfull[L.fid[ln]] = C.x;  // full primal vector in LDS
+        if (L.xfull && have_map && ln < nf) L.xfull[L.fid[ln]] = C.x;  // full primal in LDS
         wave_sync();
         if (C.status == ST_OK && ln < C.q) {
             const int id = C.act;

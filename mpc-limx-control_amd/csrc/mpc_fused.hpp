@@ -118,8 +118,9 @@ struct MpcLayout {
     //   H_FF build       : packed H at [0, HB), HB = NF(NF+1)/2, reading the condensed terms
     //   solver           : packed L / R at [0, NR), then 5 NF broadcast / 1/R(j,j) doubles
     static constexpr int oXS = 0;                         // x mirror (NF)
-    static constexpr int oXF = oXS + NF;                  // xfull (NV)
-    static constexpr int oMisc = oXF + NV;                // rowfix / ys slot
+    // no xfull: every fixed input of these models is 0 (a swing foot's forces; the literal
+    // model has none), so C.L.xfull = nullptr and the solver reads 0 (gi_solver.hpp)
+    static constexpr int oMisc = oXS + NF;                // rowfix / ys slot
     static constexpr int oCB = oMisc + 2;                 // b of the bound constraints (2 NF)
     static constexpr int oU = (oCB + 2 * NF + 1) & ~1;    // the shared region (16-B aligned)
     // early-phase view
@@ -133,7 +134,8 @@ struct MpcLayout {
     static constexpr int HB = NF * (NF + 1) / 2;
     // condensed terms, live until H_FF and g are built
     static constexpr int oS = oU + (((nEarly > HB ? nEarly : HB) + 1) & ~1);  // [NU*NU][4]
-    static constexpr int oUV = oS + 4 * NU * NU;          // u_m, v_m: [(N+1)][2][NU]
+    // u_m, v_m: [(N+1)][2][NU], m = 1..N used (slot m = 0 overlaps the end of S, never touched)
+    static constexpr int oUV = oS + 4 * NU * NU - 2 * NU;
     static constexpr int oRm = oUV + (N + 1) * 2 * NU;    // R (NU x NU) copy
     static constexpr int nMid = oRm + NU * NU - oU;
     // solver view
@@ -380,7 +382,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     C.L.J = nullptr;
     C.L.g = nullptr;
     C.L.xs = D + Lay::oXS;
-    C.L.xfull = D + Lay::oXF;
+    C.L.xfull = nullptr;  // fixed inputs are 0 (MpcLayout)
     C.L.rowfix = D + Lay::oMisc;
     C.L.ys = D + Lay::oMisc;
     int *ip = reinterpret_cast<int *>(D + Lay::nDoubles);
