@@ -373,7 +373,8 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             z4[j & 3] += Jr[j] * colb[j];
             if ((j & 7) == 7) step_fence();
         }
-        const double z = (z4[0] + z4[1]) + (z4[2] + z4[3]);
+        double z = (z4[0] + z4[1]) + (z4[2] + z4[3]);
+        pin(z);  // here, not sunk to its use after the R solve: the row would stay live
         // r = R^-1 d(0:q) (R in LDS, 1/R(j,j) kept beside it); nothing to do while q == 0
         double r = 0.0, t1 = INFINITY;
         int kslot = 0x7fffffff;

@@ -56,6 +56,8 @@ struct SolveOut {
     int *status;    // 1
     int *iters;     // 1
     double *y;      // nullable: nV + mA multipliers (qpOASES convention)
+    double *stage = nullptr;  // nullable: nV doubles of dead LDS; x is assembled there and
+                              // written once, coalesced and non-temporal
 };
 
 // LDS workspace (bytes) for a free-variable cap and dims
@@ -585,15 +587,21 @@ __device__ __forceinline__ void gi_write(GiCtx &C, const SolveOut &O) {
     GiLds &L = C.L;
     const int nV = P.nV, mA = P.mA, nf = C.nf, ln = lane(), nfric = C.nfric;
     const bool have_map = nf <= C.nfmax && nf <= kWave;
+    double *xo = O.stage ? O.stage : O.x;
+    if (O.stage) wave_sync();
     for (int v = ln; v < nV; v += kWave) {
         const int pv = L.pos[v];
-        if (pv < 0 || !have_map) O.x[v] = (pv < 0) ? xfixed(L, v) : 0.0;
+        if (pv < 0 || !have_map) xo[v] = (pv < 0) ? xfixed(L, v) : 0.0;
     }
-    if (have_map && ln < nf) O.x[L.fid[ln]] = C.x;
+    if (have_map && ln < nf) xo[L.fid[ln]] = C.x;
+    if (O.stage) {
+        wave_sync();
+        for (int v = ln; v < nV; v += kWave) stream_store(O.x + v, O.stage[v]);
+    }
     if (ln == 0) {
-        *O.cost = C.fval + C.c0;
-        *O.status = C.status;
-        *O.iters = C.iters;
+        stream_store(O.cost, C.fval + C.c0);
+        stream_store(O.status, C.status);
+        stream_store(O.iters, C.iters);
     }
     if (O.y) {
         // multipliers: y_b (nV) then y_A (mA) with H x + f = y_b + A' y_A, built in LDS

@@ -148,6 +148,7 @@ struct MpcLayout {
         sizeof(double) * nDoubles + sizeof(int) * (NF + NV) + ((MT + 15) & ~15);
     static constexpr size_t lds_bytes = (bytes + 15) & ~(size_t)15;
     static_assert(oRow % 2 == 0 && oU % 2 == 0 && oS % 2 == 0, "16-byte aligned buffers");
+    static_assert(NV <= NR, "gi_write stages x in the packed R space");
     static_assert(HB <= NR, "packed H fits the L / R space");
 };
 
@@ -206,13 +207,13 @@ __device__ __forceinline__ void mpc_load_inputs(const MpcArgs &a, int b, double 
         }
     } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) lin[i] = a.lin[(size_t)b * 8 + i];
+        for (int i = 0; i < 8; ++i) lin[i] = stream_load(a.lin + (size_t)b * 8 + i);
         constexpr int NXR = NX * (N + 1), RX = (NXR + kWave - 1) / kWave;
         const double *xrg = a.xref + (size_t)b * NXR;
         double v[RX];
 #pragma unroll
-        for (int r = 0; r < RX; ++r) v[r] = (ln + r * kWave < NXR) ? xrg[ln + r * kWave] : 0.0;
-        const double x0l = (ln < NX) ? a.x0[(size_t)b * NX + ln] : 0.0;
+        for (int r = 0; r < RX; ++r) v[r] = (ln + r * kWave < NXR) ? stream_load(xrg + ln + r * kWave) : 0.0;
+        const double x0l = (ln < NX) ? stream_load(a.x0 + (size_t)b * NX + ln) : 0.0;
         const double rml = (ln < NU * NU) ? a.rmat[ln] : 0.0;
 #pragma unroll
         for (int r = 0; r < RX; ++r)
@@ -366,7 +367,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     P.fz_min = a.fz_min; P.fz_max = a.fz_max; P.fxy_max = a.fxy_max;
     P.u_min = a.u_min; P.u_max = a.u_max;
     P.contact = (MODEL != 0) ? 0ull
-              : GEN ? gait_mask_wave(N, a.Ts, a.phase[b], a.swing, a.stance) : a.contact[b];
+              : GEN ? gait_mask_wave(N, a.Ts, a.phase[b], a.swing, a.stance) : stream_load(a.contact + b);
     P.friction = FRIC ? 1 : 0;
     P.mu = a.mu;
     P.mA = 0; P.A = nullptr; P.a_colmajor = 0; P.lbA = nullptr; P.ubA = nullptr;
@@ -506,6 +507,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     O.status = a.status + b;
     O.iters = a.iters + b;
     O.y = nullptr;
+    O.stage = C.L.R;  // the packed R is dead after the solve
     gi_write(C, O);
     MPCQP_STAMP(a.stamps, 9, tw);
     (void)NS;

@@ -86,6 +86,7 @@ struct PairLayout {
     static constexpr size_t lds_bytes = 2 * bytes;  // both halves
     static_assert(oU % 2 == 0 && oRow % 2 == 0 && oS % 2 == 0, "16-byte aligned buffers");
     static_assert(HB <= NR, "packed H fits the L / R space");
+    static_assert(NV <= NR, "the U staging row fits the L / R space");
     static_assert(N <= kHalf, "one lane per horizon step in the gait mask");
 };
 
@@ -214,16 +215,16 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         contact = gait_mask_half(N, a.Ts, ph0, a.swing, a.stance);
     } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) lin[i] = a.lin[(size_t)b * 8 + i];
+        for (int i = 0; i < 8; ++i) lin[i] = stream_load(a.lin + (size_t)b * 8 + i);
         constexpr int NXR = NX * (N + 1), RX = (NXR + kHalf - 1) / kHalf;
         const double *xrg = a.xref + (size_t)b * NXR;
         double v[RX];
 #pragma unroll
-        for (int r = 0; r < RX; ++r) v[r] = (hl + r * kHalf < NXR) ? xrg[hl + r * kHalf] : 0.0;
-        const double x0l = (hl < NX) ? a.x0[(size_t)b * NX + hl] : 0.0;
+        for (int r = 0; r < RX; ++r) v[r] = (hl + r * kHalf < NXR) ? stream_load(xrg + hl + r * kHalf) : 0.0;
+        const double x0l = (hl < NX) ? stream_load(a.x0 + (size_t)b * NX + hl) : 0.0;
         const double rm0 = (hl < NRM) ? a.rmat[hl] : 0.0;
         const double rm1 = (hl + kHalf < NRM) ? a.rmat[hl + kHalf] : 0.0;
-        if (MODEL == 0) contact = a.contact[b];
+        if (MODEL == 0) contact = stream_load(a.contact + b);
 #pragma unroll
         for (int r = 0; r < RX; ++r)
             if (hl + r * kHalf < NXR) xr[hl + r * kHalf] = v[r];
@@ -600,6 +601,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
             }
             z = sg * ((z4[0] + z4[1]) + (z4[2] + z4[3]));
+            pin(z);  // here, not sunk to its use after the R solve: the row would stay live
             // r = R^-1 d(0:q): uniform loop to the larger q of the two halves
             const int qmax = max(__builtin_amdgcn_readlane(q, 0), __builtin_amdgcn_readlane(q, kHalf));
             if (q > 0) {
@@ -772,22 +774,28 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     if (bo >= 0 && defer) {
         if (hl == 0) wg_list_append(a.ovf, bo);
     } else if (bo >= 0) {
+        // U assembled in LDS (the dead L / R space), then written once, coalesced: a
+        // non-temporal store of a partial line is its own HBM write
         const uint64_t cto = *ctl;
         double *U = a.U + (size_t)bo * NV;
+        double *Us = D + Lay::oR;
         const bool have_map = nf <= NF;
+        wave_sync();
         for (int v = hl; v < NV; v += kHalf) {
             const int pv = pos[v];
             if (pv < 0 || !have_map) {
                 double lo, hi;
                 pair_bound<NU, MODEL>(a, cto, v, lo, hi);
-                U[v] = (pv < 0) ? lo : 0.0;
+                Us[v] = (pv < 0) ? lo : 0.0;
             }
         }
-        if (have_map && hl < nf) U[fid[hl]] = x;
+        if (have_map && hl < nf) Us[fid[hl]] = x;
+        wave_sync();
+        for (int v = hl; v < NV; v += kHalf) stream_store(U + v, Us[v]);
         if (hl == 0) {
-            a.cost[bo] = fval;
-            a.status[bo] = status;
-            a.iters[bo] = iters;
+            stream_store(a.cost + bo, fval);
+            stream_store(a.status + bo, status);
+            stream_store(a.iters + bo, iters);
         }
     }
     (void)NS;

@@ -192,6 +192,29 @@ __device__ __forceinline__ double rsqrt_nr(double a) {
 // Materialise v in a VGPR at this point: arithmetic producing v cannot sink past it.
 __device__ __forceinline__ void pin(double &v) { asm volatile("" : "+v"(v)); }
 
+// Per-instance inputs and outputs are touched once: stream them past L2 (non-temporal) so they
+// do not evict the scratch lines of the waves' spilled registers, which otherwise leave L2 as
+// write-backs (MPCQP_STREAM=0: ordinary loads / stores)
+#ifndef MPCQP_STREAM
+#define MPCQP_STREAM 1
+#endif
+template <typename T>
+__device__ __forceinline__ T stream_load(const T *p) {
+#if MPCQP_STREAM
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+template <typename T>
+__device__ __forceinline__ void stream_store(T *p, T v) {
+#if MPCQP_STREAM
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
 // Diagnostic phase stamps (built only with -DMPCQP_STAMPS, lib/libmpcqp_stamps.so): cycles
 // (s_memtime) since the previous stamp are added to slot k of a global array.  The real
 // library compiles these to nothing.

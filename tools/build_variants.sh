@@ -10,8 +10,8 @@ HF="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -w -mllvm -pragma-unroll-threshol
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   ( mkdir -p "build/$name" && /opt/rocm/bin/hipcc $HF $flags -c -o "build/$name/fast_pair.o" csrc/fast_pair.hip && \
-    /opt/rocm/bin/hipcc $HF -shared -o "lib/libmpcqp_$name.so" build/rel/mpcqp_kernels.o build/rel/estimator.o \
-        build/rel/fast_srbm10.o build/rel/fast_srbm20.o build/rel/fast_literal.o "build/$name/fast_pair.o" && \
+    /opt/rocm/bin/hipcc $HF -shared -o "lib/libmpcqp_$name.so" $(ls build/rel/*.o | grep -v fast_pair.o) \
+        "build/$name/fast_pair.o" && \
     echo "$name $(/opt/rocm/bin/hipcc $HF $flags -Rpass-analysis=kernel-resource-usage --cuda-device-only -c \
         -o "/tmp/ru_$name.o" csrc/fast_pair.hip 2>&1 | grep -A10 'pairILi6ELi10ELi0ELb0' | grep -E 'VGPRs Spill' \
         | sed 's/.*remark://;s/\[-R.*//')" ) &

@@ -16,8 +16,19 @@ import statistics as st
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def counter(path, kernel):
-    v = [float(r["Counter_Value"]) for r in csv.DictReader(open(path)) if kernel in r["Kernel_Name"]]
+def kernel_tag(name):
+    """'k_mpc_pair<6, 10, 0, false>' out of the demangled signature."""
+    i = name.find("k_")
+    j = name.find(">", i)
+    return name[i:j + 1] if i >= 0 and j > i else name
+
+
+def counter(path, kernel, grid):
+    """Median counter value over the launches of exactly this kernel instantiation at this
+    grid size (other configs and the bench's side measurements launch other instantiations
+    or grids of the same kernel family)."""
+    v = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+         if kernel_tag(r["Kernel_Name"]) == kernel and int(r["Grid_Size"]) == grid]
     return st.median(v) if v else None, len(v)
 
 
@@ -27,25 +38,29 @@ def main():
     ap.add_argument("tag")
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--config", default="B")
-    ap.add_argument("--kernel", default="k_mpc")
+    ap.add_argument("--kernel", default="k_mpc_pair<6, 10, 0, false>")
+    ap.add_argument("--grid", type=int, default=None,
+                    help="threads per launch (default: 32 x batch, the pair kernel's grid)")
     a = ap.parse_args()
     out = os.path.join(ROOT, "profiles")
     stats = os.path.join(a.prof, "trace", "run_kernel_stats.csv")
     shutil.copy(stats, os.path.join(out, f"{a.tag}_kernel_stats.csv"))
     kern = {r["Name"]: dict(calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]),
                             pct=float(r["Percentage"])) for r in csv.DictReader(open(stats))}
-    fetch, nf = counter(os.path.join(a.prof, "fetch", "run_counter_collection.csv"), a.kernel)
-    write, nw = counter(os.path.join(a.prof, "write", "run_counter_collection.csv"), a.kernel)
+    grid = a.grid or 32 * a.batch
+    fetch, nf = counter(os.path.join(a.prof, "fetch", "run_counter_collection.csv"), a.kernel, grid)
+    write, nw = counter(os.path.join(a.prof, "write", "run_counter_collection.csv"), a.kernel, grid)
     traffic = None
     if fetch is not None and write is not None:
         traffic = 2.0 * fetch * 1024 + write * 1024
-    summ = dict(tag=a.tag, kernel=a.kernel, config=a.config, batch=a.batch, kernels=kern,
+    summ = dict(tag=a.tag, kernel=a.kernel, grid=grid, config=a.config, batch=a.batch, kernels=kern,
                 fetch_size_kib_median=fetch, write_size_kib_median=write, fetch_samples=nf,
                 write_samples=nw, hbm_bytes_per_launch=traffic,
                 correction="reads = 2 x FETCH_SIZE (gfx950 half-count), writes = WRITE_SIZE")
     json.dump(summ, open(os.path.join(out, f"{a.tag}_summary.json"), "w"), indent=1)
-    json.dump(dict(config=a.config, batch=a.batch, kernel=a.kernel, tag=a.tag,
-                   hbm_bytes_per_launch=traffic), open(os.path.join(out, "pmc_traffic.json"), "w"),
+    json.dump(dict(config=a.config, batch=a.batch, kernel=a.kernel, grid=grid, tag=a.tag,
+                   hbm_bytes_per_launch=traffic, read_bytes=2.0 * fetch * 1024 if fetch else None,
+                   write_bytes=write * 1024 if write else None), open(os.path.join(out, "pmc_traffic.json"), "w"),
               indent=1)
     print(json.dumps(summ, indent=1)[:1500])
 
