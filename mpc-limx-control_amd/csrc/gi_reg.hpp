@@ -496,22 +496,24 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         wave_sync();
         // ---- the pass's update of J: add -> the reflection (J_j -= beta (J . v) v_j),
         //      drop -> rotations (j, j+1) for j = 0 .. NF-2, identity where (c, s) = (1, 0)
-        if (add) {
-            if (beta != 0.0) {
-                double w4[4] = {0.0, 0.0, 0.0, 0.0};
+        //      Two independent uniform steps, not an if / else: the two arms' definitions of
+        //      Jr would meet in a phi that the register allocator resolves with a second copy
+        //      of the 2 NF registers (and spills)
+        if (__builtin_amdgcn_readfirstlane((int)(add && beta != 0.0))) {
+            double w4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                for (int j = 0; j < NF; ++j) {
-                    w4[j & 3] += Jr[j] * colb[j];
-                    if ((j & 7) == 7) step_fence();
-                }
-                const double f = beta * ((w4[0] + w4[1]) + (w4[2] + w4[3]));
-#pragma unroll
-                for (int j = 0; j < NF; ++j) {
-                    Jr[j] -= f * colb[j];
-                    if ((j & 7) == 7) step_fence();
-                }
+            for (int j = 0; j < NF; ++j) {
+                w4[j & 3] += Jr[j] * colb[j];
+                if ((j & 7) == 7) step_fence();
             }
-        } else {
+            const double f = beta * ((w4[0] + w4[1]) + (w4[2] + w4[3]));
+#pragma unroll
+            for (int j = 0; j < NF; ++j) {
+                Jr[j] -= f * colb[j];
+                if ((j & 7) == 7) step_fence();
+            }
+        }
+        if (__builtin_amdgcn_readfirstlane((int)!add)) {
 #pragma unroll
             for (int j = 0; j < NF - 1; ++j) {
                 const double c = rot[2 * j], s_ = rot[2 * j + 1];
