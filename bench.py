@@ -64,6 +64,15 @@ def algorithmic_bytes(nx: int, nu: int, N: int):
     return (nx + nx * (N + 1) + 7 + 2 * N + nV + 1) * 8 + 4
 
 
+def config_bytes(p):
+    """Per-QP algorithmic bytes of any config: x0, xref, the linearisation (8 doubles for the
+    SRBM / literal models, the NX x (NX + NU) [Ac | Bc] for a dense model), the contact word; U,
+    cost, status, iterations out."""
+    nx, nu, N = p["nx"], p["nu"], p["N"]
+    lin = nx * (nx + nu) if p["model"] == 2 else 8
+    return (nx + nx * (N + 1) + lin + 1 + nu * N + 1) * 8 + 2 * 4
+
+
 def flops_per_qp(p, mean_iters):
     fl = algorithmic_flops(p["nx"], p["nu"], p["N"])
     return fl["condense"] + fl["solve_fixed"] + fl["per_iter"] * float(mean_iters)
@@ -259,6 +268,15 @@ def time_config(config, B, seed, steps=10, warmup=2, gait=None, device=0):
         out["mfma_tflops"] = ex["mfma_flops_per_launch"] / (ms * 1e-3) / 1e12
         out["mfma_busy_frac"] = ex.get("mfma_busy_frac")
         out["pmc_source"] = f"profiles/pmc_flops_{config}.json ({ex.get('tag')})"
+    tr = _profile_json(f"pmc_traffic_{config}.json")
+    if tr and tr.get("batch") == B and gait is None and tr.get("hbm_bytes_per_launch"):
+        # HBM bytes of this kernel (2 x FETCH_SIZE + WRITE_SIZE, separate PMC passes) against
+        # its algorithmic inputs + outputs
+        alg = config_bytes(p) * B
+        out["traffic_bytes_per_launch"] = tr["hbm_bytes_per_launch"]
+        out["algorithmic_bytes_per_launch"] = alg
+        out["traffic_over_algorithmic"] = tr["hbm_bytes_per_launch"] / alg
+        out["traffic_source"] = f"profiles/pmc_traffic_{config}.json ({tr.get('tag')})"
     eng.close()
     return out
 

@@ -369,10 +369,11 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             }
         }
         const bool add = !isinf(t2) && t2 <= t1;
+        double beta = 0.0;
         if (add) {
             // ---- add p: the Householder reflection of gi_reg.hpp, v = d2 - |d2| e_q
             const double dq = dB[q];
-            double rqq = dq, vq = 0.0, beta = 0.0;
+            double rqq = dq, vq = 0.0;
             if (zq > 0.0) {
                 const double nrm = sqrt(zn);
                 rqq = nrm;
@@ -393,23 +394,6 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             ++q;
             fresh = true;
             __syncthreads();
-            if (beta != 0.0) {
-                double w4[4] = {0.0, 0.0, 0.0, 0.0};
-                const double *v = dqB + h * NH;
-#pragma unroll
-                for (int j = 0; j < NH; ++j) {
-                    w4[j & 3] += Jr[j] * v[j];
-                    if ((j & 7) == 7) step_fence();
-                }
-                part[h * RW + r] = (w4[0] + w4[1]) + (w4[2] + w4[3]);
-                __syncthreads();
-                const double f = beta * (part[r] + part[RW + r]);
-#pragma unroll
-                for (int j = 0; j < NH; ++j) {
-                    Jr[j] -= f * v[j];
-                    if ((j & 7) == 7) step_fence();
-                }
-            }
         } else {
             // ---- drop slot kslot (wave 0): shift the slots and R's columns left, then Givens
             //      back to triangular; the rotations go to LDS for J
@@ -464,6 +448,28 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
                 }
             }
             --q;
+        }
+        // ---- the pass's update of J, as two sequential workgroup-uniform steps (not the arms
+        //      of the if / else above): one definition chain of Jr, so the register allocator
+        //      keeps a single copy of it
+        if (__builtin_amdgcn_readfirstlane((int)(add && beta != 0.0))) {
+            double w4[4] = {0.0, 0.0, 0.0, 0.0};
+            const double *v = dqB + h * NH;
+#pragma unroll
+            for (int j = 0; j < NH; ++j) {
+                w4[j & 3] += Jr[j] * v[j];
+                if ((j & 7) == 7) step_fence();
+            }
+            part[h * RW + r] = (w4[0] + w4[1]) + (w4[2] + w4[3]);
+            __syncthreads();
+            const double f = beta * (part[r] + part[RW + r]);
+#pragma unroll
+            for (int j = 0; j < NH; ++j) {
+                Jr[j] -= f * v[j];
+                if ((j & 7) == 7) step_fence();
+            }
+        }
+        if (__builtin_amdgcn_readfirstlane((int)!add)) {
             // J columns: rotations (j, j+1), j = 0 .. NF-2, identity where (c, s) = (1, 0);
             // half 0 applies 0 .. NH-1 (the last one needs column NH from half 1), then half 1
             // continues from the carried column NH

@@ -62,6 +62,8 @@ def main():
     ap.add_argument("kernel")
     ap.add_argument("--top", type=int, default=5)
     ap.add_argument("--ctx", type=int, default=0)
+    ap.add_argument("--who", action="store_true",
+                    help="for the peak, each live register's nearest preceding definition")
     a = ap.parse_args()
     lines = open(a.asm).read().split("\n")
     st = next(i for i, l in enumerate(lines) if a.kernel in l
@@ -143,6 +145,12 @@ def main():
         if a.ctx:
             for j in range(ln - a.ctx, ln + a.ctx + 1):
                 print(f"   {j - st}: {lines[j].strip()[:110]}")
+        if a.who and len(seen) == 1:
+            defs = [(x["ln"], x) for x in ins if "op" in x and x["defs"]]
+            for r in sorted(live):
+                d = [(l_, x) for l_, x in defs if r in x["defs"] and l_ < ln]
+                l_, x = d[-1] if d else (None, None)
+                print(f"   v{r}: def at {l_} {x['text'][:70] if x else '?'}")
 
 
 if __name__ == "__main__":
