@@ -12,10 +12,10 @@ namespace {
 template <int NX, int NU, int N>
 __global__ void __launch_bounds__(WgShape<NU * N>::THREADS, 2) k_dense_wg(MpcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_d[];
-    for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
-        dense_mpc_one<NX, NU, N>(a, b, smem_d);
-        __syncthreads();
-    }
+    // one workgroup per QP (grid = B): no grid-stride loop, so nothing is hoisted out of a loop
+    // and kept live across the whole body
+    const int b = blockIdx.x;
+    if (b < a.B) dense_mpc_one<NX, NU, N>(a, b, smem_d);
 }
 
 template <int NX, int NU, int N>
