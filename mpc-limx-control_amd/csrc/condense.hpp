@@ -180,6 +180,7 @@ __device__ __forceinline__ void alg_comb(int nx, int ns, double *out, const doub
 
 __device__ __forceinline__ void expm_pade_solve(int nx, int ns, const double *U, const double *V,
                                                 double *D, double *E);
+__device__ __forceinline__ void pade_back_substitute(int nx, int ns, const double *D, double *X);
 
 // E = exp([[A, B],[0, 0]]) top block, A = T (nx x ns, already scaled by Ts), Eigen's degree
 // selection.  ws: 7 * nx * ns doubles of scratch.  Result written to E (nx x ns).
@@ -328,7 +329,13 @@ __device__ __forceinline__ void expm_pade_solve(int nx, int ns, const double *U,
         }
         wave_sync();
     }
-    // back substitution, lane j owns column j of X (in registers)
+    pade_back_substitute(nx, ns, D, X);
+}
+
+// U X = Y in place (X = E, nx x ns; U = the upper triangle of D), lane j owns column j of X
+// (in registers); one wave
+__device__ __forceinline__ void pade_back_substitute(int nx, int ns, const double *D, double *X) {
+    constexpr int MX = 32;
     {
         const int j = lane();
         if (j < ns) {

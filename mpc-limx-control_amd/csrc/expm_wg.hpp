@@ -55,6 +55,99 @@ __device__ __forceinline__ void wg_alg_comb(int nx, int ns, double *out, const d
     __syncthreads();
 }
 
+// The Pade quotient (expm_pade_solve, condense.hpp) by the workgroup: denom X = numer by
+// Gauss-Jordan elimination with expm_pade_solve's partial pivoting (pivot = largest |D(i, k)|,
+// lowest row on ties; l_i = D(i, k) / piv; row -= l_i pivot row), applied to every row but the
+// pivot's, so no back substitution (a latency chain of ~nx^2 / 2 dependent LDS reads and FMAs on
+// one wave) remains: X(i, :) = row i / D(i, i).  Same pivots as the LU; X differs from its
+// back substitution by rounding only.  Thread (wave w, lane j) holds column j of [D | numer'],
+// rows w, w + nw, .. in registers.  Per step: the pivot candidates of column k (lane k of each
+// wave) meet in LDS | barrier | rows k, p and column k are published | barrier | swap +
+// elimination in registers; buffers alternate between steps, so two barriers per column.
+// Needs nx <= 8 nw, nx + ns <= 64, and 352 doubles of scratch.
+__device__ __forceinline__ void wg_pade_solve(int nx, int ns, const double *U, const double *V,
+                                              double *E, double *scr, int wv, int nw) {
+    constexpr int MR = 8;
+    const int j = lane(), ncol = nx + ns;
+    const bool colok = j < ncol;
+    double *redv = scr, *redi = scr + 16, *rowP = scr + 32, *rowK = scr + 160, *colK = scr + 288;
+    double a[MR];
+#pragma unroll
+    for (int r = 0; r < MR; ++r) {
+        const int i = wv + nw * r;
+        double v = 0.0;
+        if (colok && i < nx) {
+            const int c = j < nx ? j : j - nx;
+            const int e = c * nx + i;
+            const double n = U[e] + V[e], d = -U[e] + V[e];
+            v = (j < nx) ? d : ((e / nx >= nx) ? n - d : n);
+        }
+        a[r] = v;
+    }
+    for (int k = 0; k < nx; ++k) {
+        const int b = k & 1;
+        if (j == k) {
+            double best = -1.0;
+            int bi = 0x7fffffff;
+#pragma unroll
+            for (int r = 0; r < MR; ++r) {
+                const int i = wv + nw * r;
+                if (i >= k && i < nx) {
+                    const double v = fabs(a[r]);
+                    if (v > best) { best = v; bi = i; }  // rows ascend: ties keep the lowest
+                }
+            }
+            redv[8 * b + wv] = best;
+            redi[8 * b + wv] = (double)bi;
+        }
+        __syncthreads();
+        double pv = redv[8 * b];
+        int p = (int)redi[8 * b];
+        for (int w = 1; w < nw; ++w) {
+            const double ov = redv[8 * b + w];
+            const int oi = (int)redi[8 * b + w];
+            if (ov > pv || (ov == pv && oi < p)) { pv = ov; p = oi; }
+        }
+        const int wp = p % nw, sp = p / nw, wk = k % nw, sk = k / nw;
+        if (colok) {
+#pragma unroll
+            for (int r = 0; r < MR; ++r) {
+                if (wv == wp && r == sp) rowP[64 * b + j] = a[r];
+                if (wv == wk && r == sk) rowK[64 * b + j] = a[r];
+            }
+        }
+        if (j == k) {
+#pragma unroll
+            for (int r = 0; r < MR; ++r) {
+                const int i = wv + nw * r;
+                if (i < nx) colK[32 * b + i] = a[r];
+            }
+        }
+        __syncthreads();
+        const double pk = colok ? rowP[64 * b + j] : 0.0;  // the pivot row after the swap
+        const double piv = rowP[64 * b + k];
+        const double ck = colK[32 * b + k], rk = colok ? rowK[64 * b + j] : 0.0;
+        const double rp = 1.0 / piv;  // one division per step; multipliers l_i = D(i, k) / piv
+#pragma unroll
+        for (int r = 0; r < MR; ++r) {  // branch-free: selects instead of EXEC-masked slots
+            const int i = wv + nw * r;
+            const double ci = (i == p) ? ck : colK[32 * b + (i < nx ? i : 0)];
+            double v = (i == k) ? pk : ((i == p) ? rk : a[r]);
+            const bool upd = i != k && i < nx && j > k && colok;
+            a[r] = upd ? v - (ci * rp) * pk : v;
+        }
+    }
+    // X(i, c) = row i / D(i, i); D(i, i) sits on lane i of the same wave
+#pragma unroll
+    for (int r = 0; r < MR; ++r) {
+        const int i = wv + nw * r;
+        if (i < nx) {
+            const double dii = readlane(a[r], i);
+            if (colok && j >= nx) E[(j - nx) * nx + i] = a[r] / dii;
+        }
+    }
+}
+
 // wave_expm by the workgroup (nt threads, nw waves).  T (nx x ns, scaled by Ts) is overwritten
 // when scaling; ws: 7 nx ns doubles; E: the result top block.  Every thread must call it.
 __device__ __forceinline__ void wg_expm(int nx, int ns, double *T, double *ws, double *E, int tid,
@@ -131,7 +224,11 @@ __device__ __forceinline__ void wg_expm(int nx, int ns, double *T, double *ws, d
         __syncthreads();
     }
     MPCQP_STAMP(stamps, 12, tx);
-    if (wv == 0) expm_pade_solve(nx, ns, U, V, A2, E);
+    if (nx <= 8 * nw && nx + ns <= kWave && 4 * sz >= 352) {
+        wg_pade_solve(nx, ns, U, V, E, A2, wv, nw);  // A2 .. W are dead here
+    } else {
+        if (wv == 0) expm_pade_solve(nx, ns, U, V, A2, E);
+    }
     __syncthreads();
     MPCQP_STAMP(stamps, 13, tx);
     for (int s = 0; s < squarings; ++s) {
