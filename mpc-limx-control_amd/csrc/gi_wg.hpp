@@ -197,7 +197,9 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
         const int v = L.fid[r], k = v / P.nu, c = v % P.nu, sft = c / 3;
         if (c % 3 == 2 && ((P.contact >> (2 * k + sft)) & 1ull)) fbase = 2 * nf + 4 * (k * P.nfeet + sft);
     }
+    MPCQP_SUB_INIT(tsub);
     while (!done) {
+        MPCQP_SUB(tsub, 3);
         if (fresh) {
             // ---- step 1: most violated inactive constraint (lowest id on ties)
             double best = INFINITY;
@@ -235,6 +237,7 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             if (tid == 0) us[q] = 0.0;
             fresh = false;
         }
+        MPCQP_SUB(tsub, 0);
         // ---- d = J' n_p (published J rows) and the slack of p
         int a0, a1 = -1;
         double c0, c1 = 0.0, bp;
@@ -287,6 +290,7 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             }
         }
         __syncthreads();
+        MPCQP_SUB(tsub, 0);
         const double uq = us[q];
         // ---- step 2
         if (iters >= max_iter) { status = ST_ITER_LIMIT; break; }
@@ -307,26 +311,53 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             wave_sum3(dd, zn, zq);
             if (ln == 0) { red[8 + 3 * wv] = dd; red[9 + 3 * wv] = zn; red[10 + 3 * wv] = zq; }
         }
+        MPCQP_SUB(tsub, 1);
         double r0 = 0.0, r1 = 0.0;  // wave 0: r of slots ln and ln + 64
         if (wv == 0 && q > 0) {
-            // r = R^-1 d(0:q), back substitution (R packed in LDS, 1/R(j,j) beside it)
+            // r = R^-1 d(0:q), back substitution (R packed in LDS, 1/R(j,j) beside it).  The
+            // chain from one step to the next is v_readlane -> mul -> FMA in registers: 1/R(j,j)
+            // is read out of registers too, and R's columns are prefetched two steps ahead, so
+            // no LDS latency sits on it; the FMA runs on every lane (a lane past its slot only
+            // changes a value that was already read)
             double v0 = (ln < q) ? dB[ln] : 0.0, v1 = (TWO && ln + 64 < q) ? dB[ln + 64] : 0.0;
+            const double ri0 = (ln < q) ? rinv[ln] : 0.0;
+            const double ri1 = (TWO && ln + 64 < q) ? rinv[ln + 64] : 0.0;
+            auto col0 = [&](int jj) { return (jj >= 0 && ln < jj) ? Lc[roff(jj) + ln] : 0.0; };
+            auto col1 = [&](int jj) {
+                return (TWO && jj >= 0 && ln + 64 < jj) ? Lc[roff(jj) + ln + 64] : 0.0;
+            };
             int j = q - 1;
-            double ra = (ln < j) ? Lc[roff(j) + ln] : 0.0;
-            double rb = (TWO && ln + 64 < j) ? Lc[roff(j) + ln + 64] : 0.0;
-            for (; j >= 0; --j) {
-                // prefetch column j - 1 while column j is applied
-                const double na = (j > 0 && ln < j - 1) ? Lc[roff(j - 1) + ln] : 0.0;
-                const double nb = (TWO && j > 0 && ln + 64 < j - 1) ? Lc[roff(j - 1) + ln + 64] : 0.0;
-                const double rj = (j < 64 ? readlane(v0, j) : readlane(v1, j - 64)) * rinv[j];
-                if (ln == j) r0 = rj;
-                if (ln < j) v0 -= ra * rj;
-                if constexpr (TWO) {
+            if constexpr (TWO) {
+                double ra = col0(j), na = col0(j - 1), rb = col1(j), nb = col1(j - 1);
+                for (; j >= 64; --j) {
+                    const double fa = col0(j - 2), fb = col1(j - 2);
+                    const double rj = readlane(v1, j - 64) * readlane(ri1, j - 64);
                     if (ln + 64 == j) r1 = rj;
-                    if (ln + 64 < j) v1 -= rb * rj;
+                    v0 -= ra * rj;
+                    v1 -= rb * rj;
+                    ra = na; na = fa;
+                    rb = nb; nb = fb;
                 }
-                ra = na;
-                rb = nb;
+            }
+            // four columns per block, the next block's loads issued before this block's chain
+            double cc[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) cc[t] = col0(j - t);
+            for (; j >= 0; j -= 4) {
+                double nc[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) nc[t] = col0(j - 4 - t);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int jj = j - t;
+                    if (jj >= 0) {
+                        const double rj = readlane(v0, jj) * readlane(ri0, jj);
+                        if (ln == jj) r0 = rj;
+                        v0 -= cc[t] * rj;
+                    }
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t) cc[t] = nc[t];
             }
             const double rmax = wave_max(fmax(ln < q ? fabs(r0) : 0.0, ln + 64 < q ? fabs(r1) : 0.0));
             double t1 = INFINITY;
@@ -340,6 +371,7 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             if (ln == 0) { red[16] = t1; red[17] = (double)ks; }
         }
         __syncthreads();
+        MPCQP_SUB(tsub, 2);
         const double z = part[r] + part[RW + r];
         const double dd = NWH == 2 ? red[8] + red[11] : red[8];
         const double zn = NWH == 2 ? red[9] + red[12] : red[9];
@@ -502,6 +534,8 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
         }
         __syncthreads();
     }
+    MPCQP_SUB(tsub, 3);
+    MPCQP_SUB_FLUSH(C.stamps, tsub);
     MPCQP_STAMP(C.stamps, 8, tst);
     MPCQP_CUT(C.cut, 7);
     C.status = status;

@@ -228,9 +228,29 @@ __device__ __forceinline__ void stream_store(T *p, T v) {
         }                                                                       \
     } while (0)
 #define MPCQP_STAMP_INIT(t) unsigned long long t = __builtin_amdgcn_s_memtime()
+// sub-phases inside a loop: cycles accumulate in registers (no atomic per pass) and go to
+// slots 12..15 once, after the loop
+#define MPCQP_SUB_INIT(t) \
+    unsigned long long t = __builtin_amdgcn_s_memtime(), t##_a0 = 0, t##_a1 = 0, t##_a2 = 0, t##_a3 = 0
+#define MPCQP_SUB(t, k)                                                         \
+    do {                                                                        \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();          \
+        t##_a##k += now_ - (t);                                                 \
+        (t) = now_;                                                             \
+    } while (0)
+#define MPCQP_SUB_FLUSH(ptr, t)                                                 \
+    do {                                                                        \
+        if ((ptr) && ::mpcqp::lane() == 0) {                                    \
+            atomicAdd(&(ptr)[12], t##_a0); atomicAdd(&(ptr)[13], t##_a1);      \
+            atomicAdd(&(ptr)[14], t##_a2); atomicAdd(&(ptr)[15], t##_a3);      \
+        }                                                                       \
+    } while (0)
 #else
 #define MPCQP_STAMP(ptr, k, t) ((void)0)
 #define MPCQP_STAMP_INIT(t) ((void)0)
+#define MPCQP_SUB_INIT(t) ((void)0)
+#define MPCQP_SUB(t, k) ((void)0)
+#define MPCQP_SUB_FLUSH(ptr, t) ((void)0)
 #endif
 
 // Diagnostic phase cuts (built only with -DMPCQP_CUTS, lib/libmpcqp_cuts.so): the kernel

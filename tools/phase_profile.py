@@ -16,7 +16,8 @@ import numpy as np  # noqa: E402
 
 NAMES = ["setup", "Phi/xf chains", "Qe", "H_FF", "gradient", "Cholesky", "J=L^-T",
          "unconstrained min", "dual loop", "write", "model build", "expm",
-         "  sub 12", "  sub 13", "  sub 14", "  sub 15"]
+         "  sub 12 (wg: selection, J-row publication)", "  sub 13 (wg: z = J2 d2, |d|^2)",
+         "  sub 14 (wg: R solve, t1, barrier)", "  sub 15 (wg: step, add/drop, J update)"]
 
 
 def main():
@@ -46,7 +47,7 @@ def main():
     for i, n in enumerate(NAMES):
         den = tot_cs if (i < 10 or i >= 12) else cyc[10:12].sum()
         share = cyc[i] / den if den > 0 else 0.0
-        print(f"  {i:2d} {n:18s} {cyc[i]:10.0f}  {100 * share:5.1f}%")
+        print(f"  {i:2d} {n:38s} {cyc[i]:10.0f}  {100 * share:5.1f}%")
     print(f"  condense_solve total {tot_cs:10.0f} ; discretize total {cyc[10:12].sum():10.0f}")
     eng.close()
 
