@@ -64,10 +64,10 @@ __device__ __forceinline__ void wg_alg_comb(int nx, int ns, double *out, const d
 // rows w, w + nw, .. in registers.  Per step: the pivot candidates of column k (lane k of each
 // wave) meet in LDS | barrier | rows k, p and column k are published | barrier | swap +
 // elimination in registers; buffers alternate between steps, so two barriers per column.
-// Needs nx <= 8 nw, nx + ns <= 64, and 352 doubles of scratch.
+// Needs nx <= MR nw (MR <= 8), nx + ns <= 64, and 352 doubles of scratch.
+template <int MR>  // row slots per thread: nx <= MR nw
 __device__ __forceinline__ void wg_pade_solve(int nx, int ns, const double *U, const double *V,
                                               double *E, double *scr, int wv, int nw) {
-    constexpr int MR = 8;
     const int j = lane(), ncol = nx + ns;
     const bool colok = j < ncol;
     double *redv = scr, *redi = scr + 16, *rowP = scr + 32, *rowK = scr + 160, *colK = scr + 288;
@@ -224,8 +224,10 @@ __device__ __forceinline__ void wg_expm(int nx, int ns, double *T, double *ws, d
         __syncthreads();
     }
     MPCQP_STAMP(stamps, 12, tx);
-    if (nx <= 8 * nw && nx + ns <= kWave && 4 * sz >= 352) {
-        wg_pade_solve(nx, ns, U, V, E, A2, wv, nw);  // A2 .. W are dead here
+    if (nx <= 6 * nw && nx + ns <= kWave && 4 * sz >= 352) {  // A2 .. W are dead here
+        wg_pade_solve<6>(nx, ns, U, V, E, A2, wv, nw);         // config E: 24 rows, 4 waves
+    } else if (nx <= 8 * nw && nx + ns <= kWave && 4 * sz >= 352) {
+        wg_pade_solve<8>(nx, ns, U, V, E, A2, wv, nw);
     } else {
         if (wv == 0) expm_pade_solve(nx, ns, U, V, A2, E);
     }
