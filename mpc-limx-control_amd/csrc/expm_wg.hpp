@@ -19,12 +19,28 @@ __device__ __forceinline__ void wg_alg_mul(int nx, int ns, const double *X, cons
         const int tm = t % tm_n, tn = t / tm_n;
         const int i = tm * 16 + li, j = tn * 16 + li;
         dx4 acc = {0.0, 0.0, 0.0, 0.0};
-        for (int s = 0; s < ks; ++s) {
-            const int kk = 4 * s + lk;
-            const bool kin = kk < nx;
-            const double a = (i < nx && kin) ? X[kk * nx + i] : 0.0;
-            const double b = (j < ns && kin) ? Y[j * nx + kk] : 0.0;
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+        if (ks <= 8) {  // as mfma_gemm: operands first (clamped loads + selects), then the chain
+            double av[8], bv[8];
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const int kk = 4 * s + lk;
+                const bool oka = s < ks && i < nx && kk < nx, okb = s < ks && j < ns && kk < nx;
+                const double a = X[oka ? kk * nx + i : 0];
+                const double b = Y[okb ? j * nx + kk : 0];
+                av[s] = oka ? a : 0.0;
+                bv[s] = okb ? b : 0.0;
+            }
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                if (s < ks) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
+        } else {
+            for (int s = 0; s < ks; ++s) {
+                const int kk = 4 * s + lk;
+                const bool kin = kk < nx;
+                const double a = (i < nx && kin) ? X[kk * nx + i] : 0.0;
+                const double b = (j < ns && kin) ? Y[j * nx + kk] : 0.0;
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+            }
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {

@@ -27,12 +27,31 @@ __device__ __forceinline__ void mfma_gemm(int m, int n, int k, const double *A, 
         const int tm = t % tm_n, tn = t / tm_n;
         const int i = tm * 16 + li, j = tn * 16 + li;
         dx4 acc = {0.0, 0.0, 0.0, 0.0};
-        for (int s = 0; s < ks; ++s) {
-            const int kk = 4 * s + lk;
-            const bool kin = kk < k;
-            const double a = (i < m && kin) ? (TA ? A[i * lda + kk] : A[kk * lda + i]) : 0.0;
-            const double b = (j < n && kin) ? B[j * ldb + kk] : 0.0;
-            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+        if (ks <= 8) {
+            // k <= 32 (every product of the dense path): all operands loaded first, from
+            // clamped addresses with the out-of-range ones zeroed by a select (no EXEC-masked
+            // loads, one wait), then the MFMA chain
+            double av[8], bv[8];
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const int kk = 4 * s + lk;
+                const bool oka = s < ks && i < m && kk < k, okb = s < ks && j < n && kk < k;
+                const double a = A[oka ? (TA ? i * lda + kk : kk * lda + i) : 0];
+                const double b = B[okb ? j * ldb + kk : 0];
+                av[s] = oka ? a : 0.0;
+                bv[s] = okb ? b : 0.0;
+            }
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                if (s < ks) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
+        } else {
+            for (int s = 0; s < ks; ++s) {
+                const int kk = 4 * s + lk;
+                const bool kin = kk < k;
+                const double a = (i < m && kin) ? (TA ? A[i * lda + kk] : A[kk * lda + i]) : 0.0;
+                const double b = (j < n && kin) ? B[j * ldb + kk] : 0.0;
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+            }
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
