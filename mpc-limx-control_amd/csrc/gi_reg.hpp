@@ -308,7 +308,9 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                 if (warm_bit(w, fb + t)) gmask |= 4 << t;
         }
     }
+    MPCQP_SUB_INIT(tsub);
     while (!done) {
+        MPCQP_SUB(tsub, 3);
         if (fresh) {
             // ---- step 1: most violated inactive constraint (lowest id on ties)
             double best = INFINITY;
@@ -357,7 +359,9 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             }
         }
         double dj, sp;
+        MPCQP_SUB(tsub, 0);
         gi_project_reg<NF>(C, Jr, p, x, dj, sp, rowbuf);
+        MPCQP_SUB(tsub, 1);
         // ---- step 2
         if (iters >= max_iter) { status = ST_ITER_LIMIT; break; }
         ++iters;
@@ -379,11 +383,32 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         double r = 0.0, t1 = INFINITY;
         int kslot = 0x7fffffff;
         if (q > 0) {
+            // the chain from one step to the next is v_readlane -> mul -> FMA in registers:
+            // 1/R(j,j) comes out of a register (lane j), R's columns are loaded four at a time
+            // one block ahead; the FMA runs on every lane (a lane at or past its slot only
+            // changes a value already read)
             double val = dj;
-            for (int j = q - 1; j >= 0; --j) {
-                const double rj = readlane(val, j) * rinv[j];
-                if (ln == j) r = rj;
-                if (ln < j) val -= L.R[roff(j) + ln] * rj;
+            const double ril = rinv[ln < NF ? ln : 0];
+            auto colR = [&](int jj) { return (jj >= 0 && ln < jj) ? L.R[roff(jj) + ln] : 0.0; };
+            int j = q - 1;
+            double cc[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) cc[t] = colR(j - t);
+            for (; j >= 0; j -= 4) {
+                double nc[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) nc[t] = colR(j - 4 - t);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int jj = j - t;
+                    if (jj >= 0) {
+                        const double rj = readlane(val, jj) * readlane(ril, jj);
+                        if (ln == jj) r = rj;
+                        val -= cc[t] * rj;
+                    }
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t) cc[t] = nc[t];
             }
             const double rmax = wave_max(ln < q ? fabs(r) : 0.0);
             if (ln < q && r > kRTol * rmax) { t1 = u / r; kslot = ln; }
@@ -393,6 +418,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         const double t2 = dep ? INFINITY : -sp / zn;
         const double t = t1 < t2 ? t1 : t2;
         if (isinf(t)) { status = ST_INFEASIBLE; break; }
+        MPCQP_SUB(tsub, 2);
         const double uq = readlane(u, q);
         if (!isinf(t2)) {
             if (ln < nf) { x += t * z; L.xs[ln] = x; }
@@ -525,6 +551,8 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         }
         wave_sync();
     }
+    MPCQP_SUB(tsub, 3);
+    MPCQP_SUB_FLUSH(C.stamps, tsub);
     MPCQP_STAMP(C.stamps, 8, tst); MPCQP_CUT(C.cut, 7);
     if (warm) {
         // this tick's active set, in the global numbering, for the next tick
