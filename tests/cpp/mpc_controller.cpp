@@ -11,29 +11,15 @@
 #include <cstring>
 #include <vector>
 
+#include "limxsdk/datatypes.h"      // test-only stand-ins (tests/cpp/eigen_shim)
+#include "state_estimator_fake.h"
+#ifdef MPCQP_COMPAT_MPC
+#include "MPCController.h"  // the drop-in class MPC (compat/), over the Eigen stand-in
+#else
 #include "mpcqp/mpc_controller.hpp"
+#endif
 
-namespace limxsdk {  // test stand-ins (field names as used at src/mpc_control.cpp:170-185)
-struct RobotState {
-    std::vector<float> q, dq, tau;
-};
-struct ImuData {
-    float quat[4], acc[3], gyro[3];
-};
-struct RobotCmd {
-    std::vector<float> q, dq, tau, Kp, Kd;
-};
-}  // namespace limxsdk
-
-struct RobotOdomState {  // include/state_estimator_fake.h:19-25
-    double pos[3], ori[3], quat[4], v_pos[3], v_ori[3];
-};
-
-struct FakeEstimator {  // StateEstimatorFake::get_state stand-in: returns what the test set
-    RobotOdomState s{};
-    RobotOdomState get_state() { return s; }
-};
-
+#ifndef MPCQP_COMPAT_MPC
 struct Vec3 {
     double v[3];
     Vec3(double a, double b, double c) : v{a, b, c} {}
@@ -52,6 +38,8 @@ struct Param {  // MPCParam's fields the tick reads (include/MPCParam.h:44-72)
                                   -0.2602 + 0.0 - 0.25981 - 0.2598 - 0.032};
 };
 
+#endif
+
 int main(int argc, char **argv) {
     if (argc < 6) {
         std::fprintf(stderr, "usage: mpc_controller N T lever(0 world|1 literal) ncand input.bin\n");
@@ -61,9 +49,15 @@ int main(int argc, char **argv) {
               ncand = std::atoi(argv[4]);
     FILE *fp = std::fopen(argv[5], "rb");
     if (!fp) return 3;
-    mpcqp::BasicMPC<Vec3, Param, FakeEstimator> mpc(N, false, 0);
+#ifdef MPCQP_COMPAT_MPC
+    // class MPC as the reference declares it: N = 20, world lever arms, one candidate
+    if (N != 20 || literal || ncand != 1) return 5;
+    MPC mpc;
+#else
+    mpcqp::BasicMPC<Vec3, Param, StateEstimatorFake> mpc(N, false, 0);
     mpc.lever_arms = literal ? mpcqp::LeverArms::ReferenceLiteral : mpcqp::LeverArms::World;
     for (int c = 1; c < ncand; ++c) mpc.candidate_offsets.push_back(0.0625 * c);
+#endif
     limxsdk::RobotState state;
     state.q.assign(6, 0.0f);
     limxsdk::ImuData imu{};
