@@ -7,7 +7,10 @@ support) in `config.per_config` (N = 1 only).
 
 One step = one pass of the hot path over the rank's shard, inputs resident in HBM:
   k_mpc_pair (linearise + discretise + condense + Goldfarb-Idnani solve, fused, two QPs per
-  wavefront) -> k_select_min (per-rank selection record [min key | winner's U])
+  wavefront; each wavefront mins its instances' keys into the context's selection words and the
+  batch's last workgroup writes the per-rank record [min key | winner's U]:
+  mpcqp_batch_solve_select, no selection launch; `--select separate` times the former
+  k_select_min launch instead)
   -> [N>1] ONE RCCL all-gather of the records (8 + 480 B per rank) -> k_reduce_records.
 No host synchronisation inside the step.
 
@@ -339,7 +342,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-config", action="store_true")
     ap.add_argument("--selection-dry-run", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--select", choices=("fused", "separate"), default="separate",
+                    help="selection record from the solve kernels (fused) or k_select_min")
     args = ap.parse_args()
+    fused = args.select == "fused"
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args, argv))
@@ -400,8 +406,11 @@ def main():
             d = eng.upload(batch_local)
 
             def step():
-                eng.solve(d)
-                eng.select_record(d, rec, index_base=index_base)
+                if fused:
+                    eng.solve_select(d, rec, index_base=index_base)
+                else:
+                    eng.solve(d)
+                    eng.select_record(d, rec, index_base=index_base)
                 if world > 1:
                     select_global(dist, rec, gathered, best, eng.reduce_records)
                 # world == 1: best is rec
@@ -427,10 +436,14 @@ def main():
                 continue
             e = evs[s]
             e[0].record(stream)
-            eng.solve(d)
+            if fused:  # selection record built by the solve kernels' last workgroup
+                eng.solve_select(d, rec, index_base=index_base)
+            else:
+                eng.solve(d)
             e[1].record(stream)
             e[2].record(stream)
-            eng.select_record(d, rec, index_base=index_base)
+            if not fused:
+                eng.select_record(d, rec, index_base=index_base)
             e[3].record(stream)
             if world > 1:
                 select_global(dist, rec, gathered, best, eng.reduce_records)
@@ -496,8 +509,10 @@ def main():
                             f"min-cost selection, global batch {G} split over {world} GPU(s)",
                    global_batch=G, batch_per_gpu=B, horizon=p["N"], nx=p["nx"], nu=p["nu"],
                    config=args.config, parallelism=f"dp{world}",
-                   selection="one all-gather of [key | U] records + k_reduce_records"
-                             if world > 1 else "k_select_min record (single GPU)",
+                   selection=(("record fused into the solve kernels (last workgroup)" if fused
+                               else "k_select_min record") +
+                              (" + one all-gather of [key | U] records + k_reduce_records"
+                               if world > 1 else " (single GPU)")),
                    selected=dict(index=bidx, cost=bcost))
     if rank == 0 and dry:
         cfg["dry_run"] = "selection only: synthetic costs, gloo, no solve"
@@ -509,7 +524,8 @@ def main():
         traffic, traffic_tag = pmc_traffic(args.config, B)
         cfg.update(solved_frac=solved, mean_solver_iters=float(iters.mean()),
                    fast_path=eng.fast_path,
-                   kernel_ms={eng.fused_kernel: mpc_ms, "k_select_min": sel_ms})
+                   kernel_ms={eng.fused_kernel: mpc_ms} if fused else
+                   {eng.fused_kernel: mpc_ms, "k_select_min": sel_ms})
         roof = dict(bound="mfma", compute_unit="fp64 VALU (k_mpc_pair issues no MFMA)",
                     kernel=eng.fused_kernel, achieved=achieved, peak=FP64_PEAK_TFLOPS,
                     unit="TFLOP/s", frac=achieved / FP64_PEAK_TFLOPS, traffic=traffic,

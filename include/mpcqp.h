@@ -37,6 +37,9 @@
  * mpcqp_batch_select_record       (new) per-rank selection record [key | winner's U] for the
  *                                 one-collective multi-GPU selection
  * mpcqp_reduce_records            (new) global winner from the all-gathered records
+ * mpcqp_batch_solve_select        mpcqp_batch_solve + mpcqp_batch_select_record in one pass:
+ *                                 the per-tick step of MPC::computeSupportFootForce over C
+ *                                 candidates (include/MPCController.h:178-180) with its choice
  * mpcqp_batch_solve_gait          mpcQP::mpcQP xref (include/mpcQP.h:74-97) + MPC::calculateGait
  *                                 (include/MPCController.h:61-75) on device, then the fused step
  * mpcqp_batch_select_state        (new) best gait candidate per state
@@ -215,6 +218,14 @@ int mpcqp_batch_select_min(mpcqp_ctx *ctx, int B, const double *cost, const int 
 int mpcqp_batch_select_record(mpcqp_ctx *ctx, int B, const double *cost, const int *status,
                               const double *U, int64_t index_base, int64_t *record);
 int mpcqp_reduce_records(mpcqp_ctx *ctx, int n, const int64_t *records, int64_t *best);
+/* mpcqp_batch_solve followed by mpcqp_batch_select_record, same arguments and results (the
+ * record bit-identical), without the selection launch on the fused paths: every workgroup of
+ * the solve kernel(s) mins its instances' keys into context-owned words and the batch's last
+ * workgroup writes the record.  Same ordering rule as mpcqp_batch_select_min (calls on one
+ * context stay on its stream).  Other contexts (generic path, dense model) run the two calls. */
+int mpcqp_batch_solve_select(mpcqp_ctx *ctx, int B, const double *x0, const double *xref,
+                             const double *lin, const uint64_t *contact, double *U, double *cost,
+                             int *status, int *iters, int64_t index_base, int64_t *record);
 
 /* ---- device-generated inputs, per-state selection and the closed loop ---- *
  * SRBM fast-path contexts only.  S states x C gait candidates, instance b = s*C + c.

@@ -61,7 +61,65 @@ struct MpcArgs {
     int *ovf;  // overflow list (mpc_wg.hpp) for instances beyond the kernel's free capacity
     unsigned long long *warm;  // GEN one-wave kernels: per-instance active-set words (WarmSet)
     int warm_words;
+    // fused min-cost selection (mpcqp_batch_solve_select; nullptr: off).  sel[0]: the running
+    // minimum key, sel[1]: the workgroup ticket; both re-armed by the finalizing workgroup.
+    // sel_final: this launch is the batch's last (the workgroup kernel when it runs), so its
+    // last workgroup writes the record [key | winner's U] to sel_rec.
+    unsigned long long *sel;
+    long long sel_base;
+    long long *sel_rec;
+    int sel_final;
 };
+
+// ---- fused selection (the record of k_select_min, mpcqp_kernels.hip, without its launch)
+constexpr unsigned long long kSelNone = 0x7fffffffffffffffull;
+// order-preserving bits of a float (larger float -> larger unsigned), as k_select_min
+__device__ __forceinline__ unsigned long long sel_order_bits(float c) {
+    const unsigned u = __float_as_uint(c);
+    return (u & 0x80000000u) ? (unsigned long long)(~u) : (unsigned long long)(u | 0x80000000u);
+}
+// key of a solved instance: (cost as fp32 bits) << 31 | global index; kSelNone if not solved
+__device__ __forceinline__ unsigned long long sel_key(int status, double cost, long long gi) {
+    return status == 0 ? (sel_order_bits((float)cost) << 31) | ((unsigned long long)gi & 0x7fffffffull)
+                       : kSelNone;
+}
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+// Every thread of the workgroup, after its instances' U / cost / status are stored; k (thread
+// 0's) is the workgroup's minimum key.  The key is min-ed into sel[0]; in the finalizing launch
+// the workgroup that takes the last ticket copies the winner's U row (written by any workgroup
+// of this or the previous launch: release / acquire at agent scope around the ticket) into the
+// record and re-arms sel[0] and the ticket for the next call on the stream.
+__device__ __forceinline__ void sel_commit(const MpcArgs &a, unsigned long long k, int nV) {
+    __shared__ int sel_last;
+    const int tid = (int)threadIdx.x;
+    if (tid == 0 && k != kSelNone)
+        __hip_atomic_fetch_min(&a.sel[0], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!a.sel_final) return;
+    if (tid == 0) {
+        __threadfence();
+        const unsigned t = __hip_atomic_fetch_add(reinterpret_cast<unsigned *>(&a.sel[1]), 1u,
+                                                  __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        sel_last = t == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!sel_last) return;
+    __threadfence();
+    const unsigned long long m = __hip_atomic_load(&a.sel[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool none = m == kSelNone;
+    const long long li = none ? 0 : (long long)(m & 0x7fffffffull) - (a.sel_base & 0x7fffffffll);
+    double *ru = reinterpret_cast<double *>(a.sel_rec + 1);
+    for (int e = tid; e < nV; e += (int)blockDim.x) ru[e] = none ? 0.0 : a.U[(size_t)li * nV + e];
+    if (tid == 0) {
+        a.sel_rec[0] = (long long)m;
+        __hip_atomic_store(&a.sel[0], kSelNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(reinterpret_cast<unsigned *>(&a.sel[1]), 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
 
 // overflow list layout (int): [0] count, [1] unused, [2 ..] instance ids
 constexpr int kListHead = 2;
@@ -509,6 +567,9 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     O.y = nullptr;
     O.stage = C.L.R;  // the packed R is dead after the solve
     gi_write(C, O);
+    // (a deferred instance returned above; its key comes from the workgroup kernel, which then
+    // is the finalizing launch)
+    if (a.sel) sel_commit(a, sel_key(C.status, C.fval + C.c0, a.sel_base + b), NV);
     MPCQP_STAMP(a.stamps, 9, tw);
     (void)NS;
 }

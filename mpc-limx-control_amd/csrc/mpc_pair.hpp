@@ -798,6 +798,12 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             stream_store(a.iters + bo, iters);
         }
     }
+    if (a.sel) {  // fused selection: the wave's smaller key (status and cost are per half)
+        const unsigned long long kh =
+            (bo >= 0 && !defer) ? sel_key(status, fval, a.sel_base + bo) : kSelNone;
+        const unsigned long long k0 = readlane_u64(kh, 0), k1 = readlane_u64(kh, kHalf);
+        sel_commit(a, k0 < k1 ? k0 : k1, NV);
+    }
     (void)NS;
 }
 

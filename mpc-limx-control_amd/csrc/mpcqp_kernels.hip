@@ -170,6 +170,10 @@ __device__ __forceinline__ unsigned long long order_bits(float c) {
 // counter for the next call on this context's stream.  No pre-fill launch of the key; an
 // empty batch (B = 0, one block) yields the no-valid-instance key 0x7fffffffffffffff.
 constexpr int kSelMaxBlocks = 1024;
+// the context's selection words: [0, kSelMaxBlocks) k_select_min partials, then its ticket,
+// then the fused selection's running key (armed to kSelNone) and ticket (MpcArgs::sel)
+constexpr int kFusedSel = kSelMaxBlocks + 1;
+constexpr int kSelSlots = kSelMaxBlocks + 3;
 // instances per block (4 per thread): 64 blocks at B = 65,536 take 8.6 us, 256 blocks 10.9 us
 constexpr int kSelPerBlock = 1024;
 __global__ void __launch_bounds__(256) k_select_min(int B, const double *cost, const int *status,
@@ -804,8 +808,9 @@ int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
         hipMemcpy(c->dP, m->P, sizeof(double) * nx * nx, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->dqd, qd, sizeof(double) * nx, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->dpd, pd, sizeof(double) * nx, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMalloc(&c->dsel, sizeof(unsigned long long) * (kSelMaxBlocks + 1)) != hipSuccess ||
-        hipMemset(c->dsel, 0, sizeof(unsigned long long) * (kSelMaxBlocks + 1)) != hipSuccess ||
+        hipMalloc(&c->dsel, sizeof(unsigned long long) * kSelSlots) != hipSuccess ||
+        hipMemset(c->dsel, 0, sizeof(unsigned long long) * kSelSlots) != hipSuccess ||
+        hipMemcpy(c->dsel + kFusedSel, &kSelNone, sizeof(kSelNone), hipMemcpyHostToDevice) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         mpcqp_ctx_destroy(c);
         return MPCQP_ERR_DEVICE;
@@ -1082,9 +1087,11 @@ static int launch_mpc(mpcqp_ctx *c, bool gen, int B, MpcArgs *a) {
         a->ovf = list;
     }
     const void *pk = gen ? c->fk.pair_gen : c->fk.pair;
+    a->sel_final = a->ovf ? 0 : 1;  // fused selection: the batch's last launch finalizes
     int rc = pk ? launch(pk, (B + 1) / 2, c->fk.pair_lds, c->stream, a)
                 : launch(gen ? c->fk.mpc_gen : c->fk.mpc, B, c->fk.mpc_lds, c->stream, a);
     if (rc || !a->ovf) return rc;
+    a->sel_final = 1;
     void *args[] = {a, &list, &rearm};
     const int grid = std::max(1, std::min(B, c->wg_grid));
     rc = hip_status(hipLaunchKernel(c->fk.wg, dim3(grid), dim3(c->fk.wg_threads), args, c->fk.wg_lds,
@@ -1267,6 +1274,40 @@ int mpcqp_batch_solve(mpcqp_ctx *c, int B, const double *x0, const double *xref,
     rc = mpcqp_batch_discretize(c, B, lin, c->dAB);
     if (rc) return rc;
     return mpcqp_batch_condense_solve(c, B, c->dAB, x0, xref, contact, U, cost, status, iters);
+}
+
+int mpcqp_batch_solve_select(mpcqp_ctx *c, int B, const double *x0, const double *xref,
+                             const double *lin, const uint64_t *contact, double *U, double *cost,
+                             int *status, int *iters, int64_t index_base, int64_t *record) {
+    if (!c || !record) return MPCQP_ERR_BAD_ARG;
+    if (B < 0) return MPCQP_ERR_BAD_ARG;
+    if (index_base < 0 || index_base + (int64_t)B > 0x7fffffffll) return MPCQP_ERR_BAD_DIMS;
+    hipSetDevice(c->device);
+    if (B > 0 && c->fast && !c->fk.dense) {
+        // the fused kernels min their keys into the context's selection words and the batch's
+        // last workgroup writes the record: no selection launch
+        if (!x0 || !xref || !lin || !U || !cost || !status || !iters) return MPCQP_ERR_BAD_ARG;
+        if (c->m.model == MPCQP_MODEL_SRBM && !contact) return MPCQP_ERR_BAD_ARG;
+        MpcArgs a = mpc_args(c, B);
+        a.lin = lin;
+        a.x0 = x0;
+        a.xref = xref;
+        a.contact = contact;
+        a.U = U;
+        a.cost = cost;
+        a.status = status;
+        a.iters = iters;
+        a.sel = c->dsel + kFusedSel;
+        a.sel_base = (long long)index_base;
+        a.sel_rec = reinterpret_cast<long long *>(record);
+        tbegin(c, 1);
+        const int rc = launch_mpc(c, false, B, &a);
+        tend(c, 1);
+        return rc;
+    }
+    int rc = mpcqp_batch_solve(c, B, x0, xref, lin, contact, U, cost, status, iters);
+    if (!rc) rc = mpcqp_batch_select_record(c, B, cost, status, U, index_base, record);
+    return rc;
 }
 
 int mpcqp_ctx_reserve(mpcqp_ctx *c, int B) {

@@ -27,6 +27,7 @@ EXPORTS = [
     "mpcqp_ctx_fast_path", "mpcqp_batch_discretize", "mpcqp_batch_condense_solve",
     "mpcqp_debug_phase_cycles", "mpcqp_batch_solve_host",
     "mpcqp_batch_select_min", "mpcqp_batch_select_record", "mpcqp_reduce_records",
+    "mpcqp_batch_solve_select",
     "mpcqp_enable_timing", "mpcqp_last_kernel_ms",
     "mpcqp_batch_solve_gait", "mpcqp_batch_select_state", "mpcqp_batch_plant_srbm",
     "mpcqp_rollout", "mpcqp_fk_feet", "mpcqp_kf_update", "mpcqp_ctx_reserve",
@@ -85,6 +86,7 @@ def lib():
     L.mpcqp_batch_select_min.argtypes = [vp, i, vp, vp, C.c_int64, vp]
     L.mpcqp_batch_select_record.argtypes = [vp, i, vp, vp, vp, C.c_int64, vp]
     L.mpcqp_reduce_records.argtypes = [vp, i, vp, vp]
+    L.mpcqp_batch_solve_select.argtypes = [vp, i] + [vp] * 8 + [C.c_int64, vp]
     L.mpcqp_batch_solve_gait.argtypes = [vp, i, i] + [vp] * 4 + [C.c_float, C.c_float] + [vp] * 4
     L.mpcqp_batch_select_state.argtypes = [vp, i, i] + [vp] * 6
     L.mpcqp_batch_plant_srbm.argtypes = [vp, i, i] + [vp] * 5

@@ -123,6 +123,15 @@ class BatchEngine:
             _ptr(d["contact"]), _ptr(d["U"]), _ptr(d["cost"]), _ptr(d["status"]),
             _ptr(d["iters"])))
 
+    def solve_select(self, d, rec, index_base: int = 0):
+        """solve + this shard's selection record in one pass (mpcqp_batch_solve_select): rec
+        (int64 device [1 + nV]) <- [min key | winner's U bits], as solve() + select_record()"""
+        check("mpcqp_batch_solve_select", lib().mpcqp_batch_solve_select(
+            self.ctx, d["B"], _ptr(d["x0"]), _ptr(d["xref"]), _ptr(d["lin"]),
+            _ptr(d["contact"]), _ptr(d["U"]), _ptr(d["cost"]), _ptr(d["status"]),
+            _ptr(d["iters"]), int(index_base), _ptr(rec)))
+        return rec
+
     # -- device-generated inputs and the closed loop (SURVEY.md 8f rows 1-2) ----------------
     def upload_gait(self, g: dict):
         """g: state [S,13], feet [S,6], cmd [S,2], phase [S,C] (numpy) -> device dict"""

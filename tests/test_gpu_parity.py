@@ -673,3 +673,37 @@ def test_dense_full_size_properties(gpu, orc):
     ref = orc.dense_batch(p, sub["x0"], sub["xref"], sub["lin"])
     for j, i in enumerate(idx):
         assert u_close(U1[i], ref["U"][j]), i
+
+
+@pytest.mark.parametrize("config,gait,B", [("B", None, 4097), ("B", "standing", 512),
+                                           ("C", None, 384), ("C", "mixed", 384),
+                                           ("L", None, 300), ("E", None, 64)])
+def test_solve_select_fused_record(gpu, config, gait, B):
+    """mpcqp_batch_solve_select: the record the fused kernels build (keys min-ed per workgroup,
+    the batch's last workgroup copies the winner's U; the workgroup kernel finalizes when
+    instances overflow to it) equals k_select_min's record of the same solve and the host
+    restatement, bit for bit; repeated calls re-arm (same record), index_base offsets the key.
+    E runs the two-launch fallback."""
+    import torch
+    import mpcqp
+    from mpcqp.dist import host_record
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params(config)
+    nV = p["nu"] * p["N"]
+    batch = mpcqp.make_batch(p, B, seed=41, gait=gait) if gait else mpcqp.make_batch(p, B, seed=41)
+    eng = BatchEngine(p)
+    d = _prefilled(eng, batch)
+    dev = torch.device("cuda:0")
+    for base in (0, 123_457, 0):
+        rec = torch.full((1 + nV,), -1, dtype=torch.int64, device=dev)
+        eng.solve_select(d, rec, index_base=base)
+        eng.sync()
+        got = rec.cpu().numpy()
+        cost, status, U = (d[k].cpu().numpy() for k in ("cost", "status", "U"))
+        assert np.all(status == 0)
+        np.testing.assert_array_equal(got, host_record(cost, status, U, base))
+        rec2 = torch.full((1 + nV,), -1, dtype=torch.int64, device=dev)
+        eng.select_record(d, rec2, index_base=base)
+        eng.sync()
+        np.testing.assert_array_equal(got, rec2.cpu().numpy())
+    eng.close()
