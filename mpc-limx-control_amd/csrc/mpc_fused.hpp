@@ -61,8 +61,8 @@ struct MpcArgs {
     int *ovf;  // overflow list (mpc_wg.hpp) for instances beyond the kernel's free capacity
     unsigned long long *warm;  // GEN one-wave kernels: per-instance active-set words (WarmSet)
     int warm_words;
-    // fused min-cost selection (mpcqp_batch_solve_select; nullptr: off).  sel[0]: the running
-    // minimum key, sel[1]: the workgroup ticket; both re-armed by the finalizing workgroup.
+    // fused min-cost selection (mpcqp_batch_solve_select; nullptr: off).  sel: the running
+    // minimum key's slots and the workgroup ticket (sel_commit); re-armed by the finalizer.
     // sel_final: this launch is the batch's last (the workgroup kernel when it runs), so its
     // last workgroup writes the record [key | winner's U] to sel_rec.
     unsigned long long *sel;
@@ -88,37 +88,80 @@ __device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v,
     const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), l);
     return ((unsigned long long)hi << 32) | lo;
 }
+// The running minimum lives in kSelSlots words 128 B apart (workgroup w mins into slot
+// w % kSelSlots): one address taking an atomic from each of 32,768 wavefronts serialises them
+// (~40 us per launch measured), 256 addresses do not.  The ticket follows the slots.
+constexpr int kSelSlots = 256, kSelStride = 16, kSelTickets = 16;
+// key slots, then kSelTickets ticket words and the global ticket, each on its own 128 B
+constexpr int kSelWords = (kSelSlots + kSelTickets + 1) * kSelStride;
 // Every thread of the workgroup, after its instances' U / cost / status are stored; k (thread
-// 0's) is the workgroup's minimum key.  The key is min-ed into sel[0]; in the finalizing launch
-// the workgroup that takes the last ticket copies the winner's U row (written by any workgroup
-// of this or the previous launch: release / acquire at agent scope around the ticket) into the
-// record and re-arms sel[0] and the ticket for the next call on the stream.
-__device__ __forceinline__ void sel_commit(const MpcArgs &a, unsigned long long k, int nV) {
+// 0's) is the workgroup's minimum key; wrote: it stored any instance in this launch.  In the finalizing launch the workgroup that takes the
+// last ticket reduces the slots, copies the winner's U row (written by any workgroup of this or
+// the previous launch: release / acquire at agent scope around the ticket) into the record and
+// re-arms slots and ticket for the next call on the stream.
+__device__ __forceinline__ void sel_commit(const MpcArgs &a, unsigned long long k, int nV,
+                                           bool wrote = true) {
     __shared__ int sel_last;
-    const int tid = (int)threadIdx.x;
+    __shared__ unsigned long long sel_red[16];
+    const int tid = (int)threadIdx.x, nt = (int)blockDim.x;
+    unsigned long long *slot = &a.sel[(blockIdx.x % kSelSlots) * kSelStride];
+    if (!a.sel_final) {  // no-return atomic: the wavefront does not wait for it to complete
+        if (tid == 0 && k != kSelNone)
+            __hip_atomic_fetch_min(slot, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    unsigned long long prev = 0;
     if (tid == 0 && k != kSelNone)
-        __hip_atomic_fetch_min(&a.sel[0], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!a.sel_final) return;
+        prev = __hip_atomic_fetch_min(slot, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the min has completed (its returned value is consumed) before the ticket below
+    asm volatile("" : "+v"(prev));
+    // two-level ticket: workgroup w counts into ticket word w % kSelTickets, and the one that
+    // completes its word counts into the global word (the ~1,000 workgroups of a resident grid
+    // on one address serialise for ~15 us)
+    auto tword = [&](int i) { return reinterpret_cast<unsigned *>(&a.sel[(kSelSlots + i) * kSelStride]); };
     if (tid == 0) {
-        __threadfence();
-        const unsigned t = __hip_atomic_fetch_add(reinterpret_cast<unsigned *>(&a.sel[1]), 1u,
-                                                  __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        sel_last = t == gridDim.x - 1;
+        // release this workgroup's U rows (an agent-scope fence writes L2 back: only a
+        // workgroup that stored instances in this launch pays for one)
+        if (wrote) __threadfence();
+        // relaxed RMWs: acq_rel ones at agent scope would write L2 back in every workgroup
+        const int g = (int)gridDim.x, w = (int)(blockIdx.x % kSelTickets);
+        const int words = g < kSelTickets ? g : kSelTickets;
+        const unsigned need = (unsigned)((g - w + kSelTickets - 1) / kSelTickets);
+        const unsigned t = __hip_atomic_fetch_add(tword(w), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool last = false;
+        if (t == need - 1) {
+            const unsigned u = __hip_atomic_fetch_add(tword(kSelTickets), 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
+            last = u == (unsigned)words - 1;
+        }
+        sel_last = last;
     }
     __syncthreads();
     if (!sel_last) return;
     __threadfence();
-    const unsigned long long m = __hip_atomic_load(&a.sel[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long m = kSelNone;
+    for (int sl = tid; sl < kSelSlots; sl += nt) {
+        unsigned long long *w = &a.sel[sl * kSelStride];
+        const unsigned long long v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        m = v < m ? v : m;
+        __hip_atomic_store(w, kSelNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long t = __shfl_xor(m, o, 64);
+        m = t < m ? t : m;
+    }
+    if ((tid & 63) == 0) sel_red[tid >> 6] = m;
+    __syncthreads();
+    m = sel_red[0];
+    for (int w = 1; w < (nt + 63) / 64; ++w) m = sel_red[w] < m ? sel_red[w] : m;
     const bool none = m == kSelNone;
     const long long li = none ? 0 : (long long)(m & 0x7fffffffull) - (a.sel_base & 0x7fffffffll);
     double *ru = reinterpret_cast<double *>(a.sel_rec + 1);
-    for (int e = tid; e < nV; e += (int)blockDim.x) ru[e] = none ? 0.0 : a.U[(size_t)li * nV + e];
-    if (tid == 0) {
-        a.sel_rec[0] = (long long)m;
-        __hip_atomic_store(&a.sel[0], kSelNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(reinterpret_cast<unsigned *>(&a.sel[1]), 0u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
+    for (int e = tid; e < nV; e += nt) ru[e] = none ? 0.0 : a.U[(size_t)li * nV + e];
+    if (tid <= kSelTickets)
+        __hip_atomic_store(tword(tid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) a.sel_rec[0] = (long long)m;
 }
 
 // overflow list layout (int): [0] count, [1] unused, [2 ..] instance ids

@@ -153,9 +153,11 @@ __device__ __forceinline__ void wg_mpc_grid(const MpcArgs &a, int *list, int *re
     // fused selection: thread 0 keeps the minimum key of the block's instances (their status /
     // cost are read back after the block's own stores and a barrier)
     unsigned long long kmin = kSelNone;
+    bool wrote = false;
     auto solve = [&](int b) {
         wg_mpc_one<NU, N, MODEL, FRIC, GEN, NF>(a, b, smem);
         __syncthreads();
+        wrote = true;
         if (a.sel && threadIdx.x == 0) {
             const unsigned long long k = sel_key(a.status[b], a.cost[b], a.sel_base + b);
             kmin = k < kmin ? k : kmin;
@@ -169,7 +171,7 @@ __device__ __forceinline__ void wg_mpc_grid(const MpcArgs &a, int *list, int *re
         const int count = __hip_atomic_load(&list[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (int i = blockIdx.x; i < count; i += gridDim.x) solve(list[kListHead + i]);
     }
-    if (a.sel) sel_commit(a, kmin, NU * N);
+    if (a.sel) sel_commit(a, kmin, NU * N, wrote);
 }
 
 }  // namespace mpcqp

@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <new>
+#include <vector>
 
 #include "../../include/mpcqp.h"
 
@@ -171,9 +172,10 @@ __device__ __forceinline__ unsigned long long order_bits(float c) {
 // empty batch (B = 0, one block) yields the no-valid-instance key 0x7fffffffffffffff.
 constexpr int kSelMaxBlocks = 1024;
 // the context's selection words: [0, kSelMaxBlocks) k_select_min partials, then its ticket,
-// then the fused selection's running key (armed to kSelNone) and ticket (MpcArgs::sel)
+// then the fused selection's key slots (armed to kSelNone) and ticket (MpcArgs::sel,
+// sel_commit in mpc_fused.hpp)
 constexpr int kFusedSel = kSelMaxBlocks + 1;
-constexpr int kSelSlots = kSelMaxBlocks + 3;
+constexpr int kSelCtxWords = kFusedSel + kSelWords;
 // instances per block (4 per thread): 64 blocks at B = 65,536 take 8.6 us, 256 blocks 10.9 us
 constexpr int kSelPerBlock = 1024;
 __global__ void __launch_bounds__(256) k_select_min(int B, const double *cost, const int *status,
@@ -773,6 +775,14 @@ static bool is_diag(const double *M, int n) {
     return true;
 }
 
+// initial selection words: k_select_min's partials and ticket 0, the fused key slots armed to
+// kSelNone, the fused ticket 0
+static std::vector<unsigned long long> sel_words_armed() {
+    std::vector<unsigned long long> w((size_t)kSelCtxWords, 0ull);
+    for (int s = 0; s < kSelSlots; ++s) w[(size_t)(kFusedSel + s * kSelStride)] = kSelNone;
+    return w;
+}
+
 int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
     if (!m || !out || !m->Q || !m->R || !m->P) return MPCQP_ERR_BAD_ARG;
     *out = nullptr;
@@ -808,9 +818,9 @@ int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
         hipMemcpy(c->dP, m->P, sizeof(double) * nx * nx, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->dqd, qd, sizeof(double) * nx, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(c->dpd, pd, sizeof(double) * nx, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMalloc(&c->dsel, sizeof(unsigned long long) * kSelSlots) != hipSuccess ||
-        hipMemset(c->dsel, 0, sizeof(unsigned long long) * kSelSlots) != hipSuccess ||
-        hipMemcpy(c->dsel + kFusedSel, &kSelNone, sizeof(kSelNone), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMalloc(&c->dsel, sizeof(unsigned long long) * kSelCtxWords) != hipSuccess ||
+        hipMemcpy(c->dsel, sel_words_armed().data(), sizeof(unsigned long long) * kSelCtxWords,
+                  hipMemcpyHostToDevice) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         mpcqp_ctx_destroy(c);
         return MPCQP_ERR_DEVICE;
@@ -1283,9 +1293,10 @@ int mpcqp_batch_solve_select(mpcqp_ctx *c, int B, const double *x0, const double
     if (B < 0) return MPCQP_ERR_BAD_ARG;
     if (index_base < 0 || index_base + (int64_t)B > 0x7fffffffll) return MPCQP_ERR_BAD_DIMS;
     hipSetDevice(c->device);
-    if (B > 0 && c->fast && !c->fk.dense) {
-        // the fused kernels min their keys into the context's selection words and the batch's
-        // last workgroup writes the record: no selection launch
+    if (B > 0 && c->fast && !c->fk.dense && c->fk.wg) {
+        // the fused kernels min their keys into the context's selection words and the last
+        // workgroup of the workgroup kernel (always launched after the one-wave kernel on these
+        // contexts; its resident grid takes the tickets) writes the record: no selection launch
         if (!x0 || !xref || !lin || !U || !cost || !status || !iters) return MPCQP_ERR_BAD_ARG;
         if (c->m.model == MPCQP_MODEL_SRBM && !contact) return MPCQP_ERR_BAD_ARG;
         MpcArgs a = mpc_args(c, B);
