@@ -99,11 +99,13 @@ constexpr int kSelWords = (kSelSlots + kSelTickets + 1) * kSelStride;
 // last ticket reduces the slots, copies the winner's U row (written by any workgroup of this or
 // the previous launch: release / acquire at agent scope around the ticket) into the record and
 // re-arms slots and ticket for the next call on the stream.
+// scratch: 24 words of the caller's (dead) dynamic LDS, used only by a finalizing launch -- a
+// static __shared__ here would add to every kernel's LDS and cost the one-QP kernel a wave per CU
 __device__ __forceinline__ void sel_commit(const MpcArgs &a, unsigned long long k, int nV,
-                                           bool wrote = true) {
-    __shared__ int sel_last;
-    __shared__ unsigned long long sel_red[16];
+                                           bool wrote, unsigned long long *scratch) {
     const int tid = (int)threadIdx.x, nt = (int)blockDim.x;
+    int &sel_last = *reinterpret_cast<int *>(scratch + 16);
+    unsigned long long *sel_red = scratch;
     unsigned long long *slot = &a.sel[(blockIdx.x % kSelSlots) * kSelStride];
     if (!a.sel_final) {  // no-return atomic: the wavefront does not wait for it to complete
         if (tid == 0 && k != kSelNone)
@@ -612,7 +614,8 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     gi_write(C, O);
     // (a deferred instance returned above; its key comes from the workgroup kernel, which then
     // is the finalizing launch)
-    if (a.sel) sel_commit(a, sel_key(C.status, C.fval + C.c0, a.sel_base + b), NV);
+    if (a.sel) sel_commit(a, sel_key(C.status, C.fval + C.c0, a.sel_base + b), NV, true,
+                          reinterpret_cast<unsigned long long *>(D + Lay::oR));
     MPCQP_STAMP(a.stamps, 9, tw);
     (void)NS;
 }

@@ -802,7 +802,9 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         const unsigned long long kh =
             (bo >= 0 && !defer) ? sel_key(status, fval, a.sel_base + bo) : kSelNone;
         const unsigned long long k0 = readlane_u64(kh, 0), k1 = readlane_u64(kh, kHalf);
-        sel_commit(a, k0 < k1 ? k0 : k1, NV);
+        wave_sync();  // the U staging reads are done: the L / R space is scratch again
+        sel_commit(a, k0 < k1 ? k0 : k1, NV, true,
+                   reinterpret_cast<unsigned long long *>(smem) + Lay::oR);
     }
     (void)NS;
 }

@@ -150,28 +150,34 @@ __device__ __forceinline__ void wg_mpc_one(const MpcArgs &a, int b, unsigned cha
 template <int NU, int N, int MODEL, bool FRIC, bool GEN, int NF>
 __device__ __forceinline__ void wg_mpc_grid(const MpcArgs &a, int *list, int *rearm,
                                             unsigned char *smem) {
-    // fused selection: thread 0 keeps the minimum key of the block's instances (their status /
-    // cost are read back after the block's own stores and a barrier)
-    unsigned long long kmin = kSelNone;
-    bool wrote = false;
-    auto solve = [&](int b) {
-        wg_mpc_one<NU, N, MODEL, FRIC, GEN, NF>(a, b, smem);
-        __syncthreads();
-        wrote = true;
-        if (a.sel && threadIdx.x == 0) {
-            const unsigned long long k = sel_key(a.status[b], a.cost[b], a.sel_base + b);
-            kmin = k < kmin ? k : kmin;
-        }
-    };
     if (!list) {
-        for (int b = blockIdx.x; b < a.B; b += gridDim.x) solve(b);
-    } else {
-        if (blockIdx.x == 0 && threadIdx.x == 0)
-            __hip_atomic_store(rearm, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int count = __hip_atomic_load(&list[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        for (int i = blockIdx.x; i < count; i += gridDim.x) solve(list[kListHead + i]);
+        for (int b = blockIdx.x; b < a.B; b += gridDim.x) {
+            wg_mpc_one<NU, N, MODEL, FRIC, GEN, NF>(a, b, smem);
+            __syncthreads();
+        }
+        return;
     }
-    if (a.sel) sel_commit(a, kmin, NU * N, wrote);
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(rearm, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int count = __hip_atomic_load(&list[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = blockIdx.x; i < count; i += gridDim.x) {
+        wg_mpc_one<NU, N, MODEL, FRIC, GEN, NF>(a, list[kListHead + i], smem);
+        __syncthreads();
+    }
+    if (a.sel) {
+        // fused selection (list mode: the launch after the one-wave kernel): thread 0 reads
+        // back the keys of the block's instances (its own stores, gi_write_wg) once the solves
+        // are done; the solves' LDS is dead, the finalizer's scratch
+        unsigned long long kmin = kSelNone;
+        if (threadIdx.x == 0)
+            for (int i = blockIdx.x; i < count; i += gridDim.x) {
+                const int b = list[kListHead + i];
+                const unsigned long long k = sel_key(a.status[b], a.cost[b], a.sel_base + b);
+                kmin = k < kmin ? k : kmin;
+            }
+        sel_commit(a, kmin, NU * N, (int)blockIdx.x < count,
+                   reinterpret_cast<unsigned long long *>(smem));
+    }
 }
 
 }  // namespace mpcqp

@@ -86,7 +86,8 @@ def lib():
     L.mpcqp_batch_select_min.argtypes = [vp, i, vp, vp, C.c_int64, vp]
     L.mpcqp_batch_select_record.argtypes = [vp, i, vp, vp, vp, C.c_int64, vp]
     L.mpcqp_reduce_records.argtypes = [vp, i, vp, vp]
-    L.mpcqp_batch_solve_select.argtypes = [vp, i] + [vp] * 8 + [C.c_int64, vp]
+    if hasattr(L, "mpcqp_batch_solve_select"):  # absent from A/B builds of older sources
+        L.mpcqp_batch_solve_select.argtypes = [vp, i] + [vp] * 8 + [C.c_int64, vp]
     L.mpcqp_batch_solve_gait.argtypes = [vp, i, i] + [vp] * 4 + [C.c_float, C.c_float] + [vp] * 4
     L.mpcqp_batch_select_state.argtypes = [vp, i, i] + [vp] * 6
     L.mpcqp_batch_plant_srbm.argtypes = [vp, i, i] + [vp] * 5
