@@ -798,7 +798,10 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             stream_store(a.iters + bo, iters);
         }
     }
-    if (a.sel) {  // fused selection: the wave's smaller key (status and cost are per half)
+#ifndef MPCQP_FUSED_SEL
+#define MPCQP_FUSED_SEL 1
+#endif
+    if (MPCQP_FUSED_SEL && a.sel) {  // fused selection: the wave's smaller key (per-half status / cost)
         const unsigned long long kh =
             (bo >= 0 && !defer) ? sel_key(status, fval, a.sel_base + bo) : kSelNone;
         const unsigned long long k0 = readlane_u64(kh, 0), k1 = readlane_u64(kh, kHalf);
