@@ -238,7 +238,7 @@ __device__ __forceinline__ void dense_mpc_one(const MpcArgs &a, int b, unsigned 
     for (int r0 = 0; r0 < NV; r0 += 16) {
         const int nrow = NV - r0 < 16 ? NV - r0 : 16;
         const int ncol = ((r0 + nrow - 1) / NU + 1) * NU;  // columns a NU + c with a <= k_r
-        mfma_gemm<false>(nrow, ncol, NX, Y + r0, LY, Phi, LD, stg, LS, nullptr, 0, 1.0, wv, 0, 4);
+        mfma_gemm<false, false>(nrow, ncol, NX, Y + r0, LY, Phi, LD, stg, LS, nullptr, 0, 1.0, wv, 0, 4);
         __syncthreads();
         if (ok && r >= r0 && r < r0 + nrow && r < nf) {
             const int kr = r / NU, cr = r % NU;

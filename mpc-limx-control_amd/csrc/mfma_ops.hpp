@@ -15,7 +15,9 @@ typedef double dx4 __attribute__((ext_vector_type(4)));
 // and are not stored.  Operand maps of the f64 16x16x4 form (cdna_hip_programming.md section
 // 3): lane l supplies A(row l & 15, k = 4s + (l >> 4)) and B(k = 4s + (l >> 4), col l & 15);
 // accumulator register r holds D(row (l >> 4) + 4r, col l & 15).  C must not alias A, B or D.
-template <bool TA>
+// BATCH: load all of a tile's operands before its MFMA chain (k <= 32); off where registers
+// are scarce (the H-row staging holds each thread's row part live across the product)
+template <bool TA, bool BATCH = true>
 __device__ __forceinline__ void mfma_gemm(int m, int n, int k, const double *A, int lda,
                                           const double *B, int ldb, double *C, int ldc,
                                           const double *D, int ldd, double alpha, int wv, int w0,
@@ -27,7 +29,7 @@ __device__ __forceinline__ void mfma_gemm(int m, int n, int k, const double *A, 
         const int tm = t % tm_n, tn = t / tm_n;
         const int i = tm * 16 + li, j = tn * 16 + li;
         dx4 acc = {0.0, 0.0, 0.0, 0.0};
-        if (ks <= 8) {
+        if (BATCH && ks <= 8) {
             // k <= 32 (every product of the dense path): all operands loaded first, from
             // clamped addresses with the out-of-range ones zeroed by a select (no EXEC-masked
             // loads, one wait), then the MFMA chain
