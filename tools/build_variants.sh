@@ -6,7 +6,7 @@
 # compiler's VGPR spill count for the config B kernel.
 R=$(cd "$(dirname "$0")/.." && pwd)
 cd "$R/mpc-limx-control_amd" || exit 1
-HF="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -w -mllvm -pragma-unroll-threshold=1000000"
+HF="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -w -mllvm -pragma-unroll-threshold=1000000 -mllvm -amdgpu-sched-strategy=max-ilp"
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   ( mkdir -p "build/$name" && /opt/rocm/bin/hipcc $HF $flags -c -o "build/$name/fast_pair.o" csrc/fast_pair.hip && \
