@@ -1,0 +1,17 @@
+#!/bin/bash
+# Stall / issue counters of the headline kernel (two --pmc passes of <= 8 SQ counters each;
+# never combined with trace domains).  Usage (GPU box, repo root): tools/pmc_stall.sh OUT
+set -o pipefail
+OUT=${1:-gpurun_out/stall}
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-per-config"
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+R=$(pwd)
+i=0
+for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
+           "SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA"; do
+    i=$((i+1))
+    timeout -s KILL 90 rocprofv3 --pmc $grp -d "$R/$OUT/g$i" -o run --output-format csv \
+        -- python3 bench.py $ARGS > "$OUT/g$i.log" 2>&1 || { echo "group $i failed: $grp"; tail -3 "$OUT/g$i.log"; }
+done
+echo stall done
