@@ -420,12 +420,14 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
                     rinv[q] = 1.0 / rqq;
                     acts[q] = p;
                     L.st[p] = 2;
-                    dqB[q] = vq;
                 }
             }
+            // the reflector's slot q: written by every wave for its own J update below (LDS is
+            // in order within a wave, and no wave reads dqB between the barrier after the R
+            // solve and that update), so the add step needs no workgroup barrier of its own
+            if (ln == 0) dqB[q] = vq;
             ++q;
             fresh = true;
-            __syncthreads();
         } else {
             // ---- drop slot kslot (wave 0): shift the slots and R's columns left, then Givens
             //      back to triangular; the rotations go to LDS for J
@@ -492,9 +494,11 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
                 w4[j & 3] += Jr[j] * v[j];
                 if ((j & 7) == 7) step_fence();
             }
-            part[h * RW + r] = (w4[0] + w4[1]) + (w4[2] + w4[3]);
+            // partial sums into d2B / tB (dead on the add path), not part: a lagging wave may
+            // still be reading this pass's z out of part
+            (h ? tB : d2B)[r] = (w4[0] + w4[1]) + (w4[2] + w4[3]);
             __syncthreads();
-            const double f = beta * (part[r] + part[RW + r]);
+            const double f = beta * (d2B[r] + tB[r]);
 #pragma unroll
             for (int j = 0; j < NH; ++j) {
                 Jr[j] -= f * v[j];
