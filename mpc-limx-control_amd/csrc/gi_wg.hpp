@@ -328,15 +328,31 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             };
             int j = q - 1;
             if constexpr (TWO) {
-                double ra = col0(j), na = col0(j - 1), rb = col1(j), nb = col1(j - 1);
-                for (; j >= 64; --j) {
-                    const double fa = col0(j - 2), fb = col1(j - 2);
-                    const double rj = readlane(v1, j - 64) * readlane(ri1, j - 64);
-                    if (ln + 64 == j) r1 = rj;
-                    v0 -= ra * rj;
-                    v1 -= rb * rj;
-                    ra = na; na = fa;
-                    rb = nb; nb = fb;
+                // slots >= 64: four columns per block as below (one wave per SIMD at NF = 128,
+                // so the LDS latency of a two-step prefetch sat on the chain); a block's steps
+                // below 64 are left to the loop after it, which restarts at column 63
+                if (j >= 64) {
+                    double ca[4], cb[4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) { ca[t] = col0(j - t); cb[t] = col1(j - t); }
+                    for (; j >= 64; j -= 4) {
+                        double na[4], nb[4];
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) { na[t] = col0(j - 4 - t); nb[t] = col1(j - 4 - t); }
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const int jj = j - t;
+                            if (jj >= 64) {
+                                const double rj = readlane(v1, jj - 64) * readlane(ri1, jj - 64);
+                                if (ln + 64 == jj) r1 = rj;
+                                v0 -= ca[t] * rj;
+                                v1 -= cb[t] * rj;
+                            }
+                        }
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) { ca[t] = na[t]; cb[t] = nb[t]; }
+                    }
+                    j = 63;
                 }
             }
             // four columns per block, the next block's loads issued before this block's chain
