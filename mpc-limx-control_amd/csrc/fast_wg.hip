@@ -12,7 +12,7 @@ namespace {
 
 // one 4-wave workgroup per QP; list != nullptr: the overflow list, else the whole batch
 template <int NU, int N, int MODEL, bool FRIC, bool GEN, int NF>
-__global__ void __launch_bounds__(WgShape<NF>::THREADS, (NF <= 64 ? 3 : 1))
+__global__ void __launch_bounds__(WgShape<NF>::THREADS, (NF <= 64 ? 2 : 1))
     k_mpc_wg(MpcArgs a, int *list, int *rearm) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_w[];
     wg_mpc_grid<NU, N, MODEL, FRIC, GEN, NF>(a, list, rearm, smem_w);
