@@ -203,6 +203,46 @@ def host_staged_rate(eng, batch, p, reps=5):
     return B * reps / (time.perf_counter() - t)
 
 
+def per_tick_latency(p, seed, ticks=1000, warmup=50, device=0):
+    """The controller's real path: one MPC tick host-to-host, as
+    ConvexMpc::solve / MPC::computeSupportFootForce make it (include/mpcqp/convex_mpc.hpp ->
+    mpcqp_batch_solve_host: host arrays in, the fused step, U / cost / status / iterations back,
+    synchronous), for 1 state x {1, 16} gait candidates, against the 1 ms control period
+    (include/MPCParam.h:44).  ctypes adds ~1 us per call over the C++ caller."""
+    import ctypes as C
+
+    import mpcqp
+    from mpcqp._lib import lib
+    from mpcqp.engine import BatchEngine
+    out = dict(path="mpcqp_batch_solve_host (ConvexMpc::solve), host arrays in/out, synchronous",
+               period_us=1000.0, ticks=ticks)
+    eng = BatchEngine(p, device=device)
+    eng.reserve(CANDIDATES)
+    nV = p["nu"] * p["N"]
+    full = mpcqp.make_batch(p, CANDIDATES, seed=seed)
+    for Cn in (1, CANDIDATES):
+        ins = [np.ascontiguousarray(full[k][:Cn]) for k in ("x0", "xref", "lin", "contact")]
+        U = np.zeros(Cn * nV)
+        cost = np.zeros(Cn)
+        st = np.zeros(Cn, np.int32)
+        it = np.zeros(Cn, np.int32)
+        args = [eng.ctx, Cn] + [C.c_void_p(a.ctypes.data) for a in ins + [U, cost, st, it]]
+        fn = lib().mpcqp_batch_solve_host
+        for _ in range(warmup):
+            assert fn(*args) == 0
+        ts = np.empty(ticks)
+        for i in range(ticks):
+            t0 = time.perf_counter_ns()
+            fn(*args)
+            ts[i] = (time.perf_counter_ns() - t0) * 1e-3
+        assert np.all(st == 0)
+        out[f"C{Cn}"] = dict(p50_us=float(np.percentile(ts, 50)), p99_us=float(np.percentile(ts, 99)),
+                             mean_us=float(ts.mean()), max_us=float(ts.max()),
+                             max_solver_iters=int(it.max()))
+    eng.close()
+    return out
+
+
 def gait_fused_rate(eng, p, B, seed, reps=10):
     """QP/s of mpcqp_batch_solve_gait: the same step with x0/xref/lin/contact generated on
     chip from per-state data (B/16 states x 16 gait candidates)."""
@@ -340,6 +380,8 @@ def main():
     ap.add_argument("--seed", type=int, default=20250404)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-config", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="skip the per-kernel timing pass after the timed steps")
     ap.add_argument("--selection-dry-run", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--select", choices=("fused", "separate"), default="separate",
                     help="selection record from the solve kernels (fused) or k_select_min")
@@ -457,15 +499,29 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         mpc_ms = sel_ms = None
+        kern = {}
         if not dry:
             mpc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
             sel_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
+            if not args.no_kernel_timing:
+                # each kernel alone: HIP events inside the library around each launch (on the ctx
+                # stream; slot 2 the one-wave fused kernel, 3 the overflow workgroup kernel), over
+                # `steps` more steps right after the timed ones -- event records between the two
+                # kernels cost ~25 us per step, so they stay out of the timed region
+                eng.enable_timing(True)
+                for _ in range(steps):
+                    step()
+                sync()
+                for w, name in ((2, eng.fused_kernel), (3, "k_mpc_wg")):
+                    ms, n = eng.kernel_ms_sum(w)
+                    if n:
+                        kern[name] = dict(ms=ms / n, launches=n)
+                eng.enable_timing(False)
             status = d["status"].cpu().numpy()
             iters = d["iters"].cpu().numpy()
         else:
             status, iters = batch_local["status"], np.zeros(Bl, np.int32)
-        return elapsed, mpc_ms, sel_ms, best.cpu().numpy(), status, iters, eng, \
-            (batch_local if dry else None)
+        return elapsed, mpc_ms, sel_ms, best.cpu().numpy(), status, iters, eng, kern
 
     # ---- strong scaling: the global batch split over the ranks (the metric) ----------------
     if dry:
@@ -475,7 +531,7 @@ def main():
         full = mpcqp.make_batch(p, G, seed=args.seed)
         local_batch = slice_batch(full, i0, B)
         del full
-    elapsed, mpc_ms, sel_ms, best, status, iters, eng, _ = run_line(
+    elapsed, mpc_ms, sel_ms, best, status, iters, eng, kern = run_line(
         local_batch, i0, args.steps, args.warmup)
     bcost, bidx, bU = decode_record(best)
 
@@ -519,14 +575,22 @@ def main():
         print(json.dumps(out), flush=True)
     elif rank == 0:
         f_qp = flops_per_qp(p, iters.mean())
-        achieved = f_qp * B / (mpc_ms * 1e-3) / 1e12
+        # the dominant kernel's own launches (library events around it); the events around the
+        # whole solve in the timed steps (mpc_ms) also hold the overflow launch
+        k_ms = kern[eng.fused_kernel]["ms"] if eng.fused_kernel in kern else mpc_ms
+        achieved = f_qp * B / (k_ms * 1e-3) / 1e12
         traffic, traffic_tag = pmc_traffic(args.config, B)
+        kms = {k: v["ms"] for k, v in kern.items()}
+        kms["mpcqp_batch_solve" + ("_select" if fused else "") +
+            " (timed steps, events around the call)"] = mpc_ms
+        if not fused:
+            kms["k_select_min"] = sel_ms
         cfg.update(solved_frac=solved, mean_solver_iters=float(iters.mean()),
-                   fast_path=eng.fast_path,
-                   kernel_ms={eng.fused_kernel: mpc_ms} if fused else
-                   {eng.fused_kernel: mpc_ms, "k_select_min": sel_ms})
-        roof = dict(bound="mfma", compute_unit="fp64 VALU (k_mpc_pair issues no MFMA)",
-                    kernel=eng.fused_kernel, achieved=achieved, peak=FP64_PEAK_TFLOPS,
+                   fast_path=eng.fast_path, select=args.select, kernel_ms=kms,
+                   kernel_launches={k: v["launches"] for k, v in kern.items()})
+        roof = dict(bound="fp64-valu", compute_unit="fp64 VALU (k_mpc_pair issues no MFMA)",
+                    kernel=eng.fused_kernel, kernel_ms=k_ms, achieved=achieved,
+                    peak=FP64_PEAK_TFLOPS,
                     unit="TFLOP/s", frac=achieved / FP64_PEAK_TFLOPS, traffic=traffic,
                     traffic_source=(f"profiles/{traffic_tag}_summary.json (rocprofv3 PMC, "
                                     "2 x FETCH_SIZE + WRITE_SIZE)") if traffic else None,
@@ -540,7 +604,7 @@ def main():
         ex = pmc_executed(args.config, B)
         if ex:
             per_launch = ex["executed_flops_per_launch"]
-            roof["executed_tflops"] = per_launch / (mpc_ms * 1e-3) / 1e12
+            roof["executed_tflops"] = per_launch / (k_ms * 1e-3) / 1e12
             roof["pipe_frac"] = roof["executed_tflops"] / FP64_PEAK_TFLOPS
             roof["executed_source"] = f"profiles/{ex.get('file', 'pmc_flops.json')} " \
                                       "(64 lanes x SQ_INSTS_VALU_FLOPS_FP64, a per-wave-" \
@@ -553,6 +617,7 @@ def main():
         if world == 1:
             cfg["pcie_inclusive_qps"] = host_staged_rate(eng, local_batch, p)
             cfg["gait_fused_qps"] = gait_fused_rate(eng, p, B, args.seed)
+            cfg["per_tick_latency"] = per_tick_latency(p, args.seed, device=local)
         out["config"] = cfg
         eng.close()
         if world == 1 and not args.no_per_config:

@@ -285,10 +285,15 @@ int mpcqp_kf_update(void *stream, int R, double dt, double *xhat, double *P, con
                     const double *acc);
 
 /* duration of the last stage-1 (which = 0: discretize / generic condense) or stage-2
- * (which = 1: condense_solve / generic solve) kernel, HIP events on the ctx stream (ms; -1 if
- * none recorded).  Timing is off until enabled. */
+ * (which = 1: condense_solve / generic solve; the whole mpcqp_batch_solve) launch, HIP events on
+ * the ctx stream (ms; -1 if none recorded).  On the fused path which = 2 times the one-wave kernel
+ * alone (k_mpc_pair / k_mpc) and which = 3 the overflow workgroup kernel (k_mpc_wg) launched
+ * after it.  Timing is off until enabled. */
 int mpcqp_enable_timing(mpcqp_ctx *ctx, int on);
 double mpcqp_last_kernel_ms(mpcqp_ctx *ctx, int which);
+/* sum (ms) over the launches of slot `which` recorded since the previous call (at most the last
+ * 64; *count receives how many), waiting for them; resets the slot's count.  -1 on error. */
+double mpcqp_kernel_ms_sum(mpcqp_ctx *ctx, int which, int *count);
 
 /* Diagnostics: per-phase cycle totals (s_memtime) of the fused kernels since the last call,
  * recorded only by the diagnostic build lib/libmpcqp_stamps.so (first call arms it); the

@@ -59,6 +59,7 @@ struct MpcArgs {
     int cands;
     float swing, stance;  // MPCParam::swing_time / stance_time (float, include/MPCParam.h:48-49)
     int *ovf;  // overflow list (mpc_wg.hpp) for instances beyond the kernel's free capacity
+    int ovf_cap;  // ids per sub-list (ovf_list_cap)
     unsigned long long *warm;  // GEN one-wave kernels: per-instance active-set words (WarmSet)
     int warm_words;
     // fused min-cost selection (mpcqp_batch_solve_select; nullptr: off).  sel: the running
@@ -166,11 +167,57 @@ __device__ __forceinline__ void sel_commit(const MpcArgs &a, unsigned long long 
     if (tid == 0) a.sel_rec[0] = (long long)m;
 }
 
-// overflow list layout (int): [0] count, [1] unused, [2 ..] instance ids
-constexpr int kListHead = 2;
-__device__ __forceinline__ void wg_list_append(int *list, int b) {
-    const int i = __hip_atomic_fetch_add(&list[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    list[kListHead + i] = b;
+// Overflow list (int words).  One counter per 128 B line would still take one device-scope
+// atomic per deferred wavefront on a single address, and those serialise (65,536 of them cost
+// ~330 us per launch at B standing).  So the list is kListSubs sub-lists: wavefront w appends
+// to sub-list w % kListSubs with ONE atomic for its deferred instances (both halves of a paired
+// wave at once).  Layout: counter of sub-list s at word s * kListStride (its own 128 B line),
+// then the sub-lists' ids, sub-list s at kListHeadWords + s * cap.  A wavefront appends at most
+// two ids, so cap = ceil(B / kListSubs) + 2 (ovf_list_cap) holds every sub-list.
+constexpr int kListSubs = 64, kListStride = 32;
+constexpr int kListHeadWords = kListSubs * kListStride;
+__host__ __device__ constexpr int ovf_list_cap(long long B) {
+    return (int)((B + kListSubs - 1) / kListSubs) + 2;
+}
+// called by one lane: append ids b0 (if d0) and b1 (if d1) to this wavefront's sub-list
+__device__ __forceinline__ void wg_list_append(int *list, int cap, int b0, bool d0, int b1,
+                                               bool d1) {
+    const int n = (d0 ? 1 : 0) + (d1 ? 1 : 0);
+    if (!n) return;
+    const int s = (int)(blockIdx.x % kListSubs);
+    const int i = __hip_atomic_fetch_add(&list[s * kListStride], n, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    int *ids = list + kListHeadWords + s * cap + i;
+    if (d0) *ids++ = b0;
+    if (d1) *ids = b1;
+}
+// the reader's view (k_mpc_wg, every wavefront alike): lane l holds sub-list l's count and the
+// inclusive prefix sum, so entry i of the concatenated list is one ballot away
+struct OvfView {
+    int *list;
+    int cap, cnt, incl, total;
+    __device__ __forceinline__ int id(int i) const {  // wave-uniform i < total
+        const int s = __popcll(__ballot(incl <= i));
+        const int excl = __shfl(incl - cnt, s, kWave);
+        return list[kListHeadWords + s * cap + (i - excl)];
+    }
+};
+__device__ __forceinline__ OvfView ovf_view(int *list, int cap) {
+    static_assert(kListSubs == kWave, "one sub-list per lane");
+    OvfView v;
+    v.list = list;
+    v.cap = cap;
+    v.cnt = __hip_atomic_load(&list[lane() * kListStride], __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+    int x = v.cnt;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const int y = __shfl_up(x, o, kWave);
+        if (lane() >= o) x += y;
+    }
+    v.incl = x;
+    v.total = __builtin_amdgcn_readlane(x, kWave - 1);
+    return v;
 }
 
 // Gait contact mask of one horizon: MPC::calculateGait (include/MPCController.h:61-75)
@@ -504,7 +551,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     if (C.nf > a.max_free) C.status = ST_BAD_DIMS;
     wave_sync();
     if (a.ovf && C.nf > NF && C.nf <= a.max_free) {  // the workgroup kernel takes it
-        if (ln == 0) wg_list_append(a.ovf, b);
+        if (ln == 0) wg_list_append(a.ovf, a.ovf_cap, b, true, 0, false);
         return;
     }
     MPCQP_STAMP(a.stamps, 0, tst);

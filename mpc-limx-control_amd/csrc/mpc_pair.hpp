@@ -50,6 +50,11 @@ namespace mpcqp {
 #ifndef MPCQP_CHOL_PF
 #define MPCQP_CHOL_PF 4
 #endif
+// the dual loop keeps R^-1 instead of R (r = R^-1 d as a lane-parallel product, no serial
+// back substitution); 0 keeps R (A/B builds)
+#ifndef MPCQP_PAIR_RINV
+#define MPCQP_PAIR_RINV 1
+#endif
 
 constexpr int kPairNF = 30;  // free variables per instance; lane 31 of a half carries g
 
@@ -168,6 +173,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     using Lay = PairLayout<NU, N, MODEL>;
     using Sup = XSupport<MODEL>;
     constexpr int NX = 13, NS = NX + NU, NF = kPairNF, NV = Lay::NV, SD = Lay::SD, NP = kHalf;
+    MPCQP_STAMP_INIT(tst);
     const int ln = lane(), hl = ln & (kHalf - 1);
     const bool up = ln >= kHalf;
     int bq = 2 * (int)blockIdx.x + (up ? 1 : 0);
@@ -235,48 +241,6 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     wave_sync();
     MPCQP_CUT(a.cut, 11);
 
-    // ---- model: lane i < NX holds row i of Ac; X0 = Bc Ts and X1 = (Ac Ts) X0 on their
-    //      support rows, A x0, A^2 x0 (A = Ac Ts).  Same products, in the same order, as the
-    //      one-QP kernel (the zero terms it adds are exact).
-    double Iwi[9];
-    double cy = 1.0, sy = 0.0;
-    if (MODEL == 0) srbm_rot_inertia(lin[0], a.Ibinv, cy, sy, Iwi);
-    auto entry = [&](int i, int j) -> double {  // [Ac | Bc](i, j)
-        return MODEL == 0 ? srbm_entry(i, j, lin, cy, sy, Iwi, a.mass)
-                          : literal_entry(i, j, lin, a.mass);
-    };
-    const double Ts = a.Ts;
-    double arow[NX];
-#pragma unroll
-    for (int k = 0; k < NX; ++k) arow[k] = entry(hl, k);
-    if (hl >= Sup::x0lo && hl < Sup::x0hi) {
-#pragma unroll
-        for (int c = 0; c < NU; ++c) X0[c * SD + hl - Sup::x0lo] = entry(hl, NX + c) * Ts;
-    }
-    if (hl < NX) {
-        double s = 0.0;
-#pragma unroll
-        for (int k = 0; k < NX; ++k) s += arow[k] * x0g[k];
-        Ax[hl] = s * Ts;
-    }
-    wave_sync();
-    if (hl >= Sup::x1lo && hl < Sup::x1hi) {
-#pragma unroll
-        for (int c = 0; c < NU; ++c) {
-            double s = 0.0;
-#pragma unroll
-            for (int k = Sup::x0lo; k < Sup::x0hi; ++k) s += arow[k] * X0[c * SD + k - Sup::x0lo];
-            X1[c * SD + hl - Sup::x1lo] = s * Ts;
-        }
-    }
-    if (hl < NX) {
-        double s = 0.0;
-#pragma unroll
-        for (int k = 0; k < NX; ++k) s += arow[k] * Ax[k];
-        A2x[hl] = s * Ts;
-    }
-    MPCQP_CUT(a.cut, 13);
-
     // ---- free map and constraint states (gi_setup for generated bounds, no rows)
     int status = ST_OK, nf = 0;
     {
@@ -305,40 +269,88 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         ctl[1] = (uint64_t)(valid ? bq : -1);
     }
     wave_sync();
+    // a wavefront whose two instances both go elsewhere (deferred to the workgroup kernel,
+    // infeasible, no free variable, past the batch) skips the model and condensed terms
+    const bool work = __ballot(valid && status == ST_OK && nf > 0) != 0ull;
+    MPCQP_STAMP(a.stamps, 0, tst);
     MPCQP_CUT(a.cut, 1);
-
-    // ---- S^W_rr = X_r' W X_r over the support rows (w: 0 = Q, 1 = P), entry o = cj NU + ci
-#pragma unroll
-    for (int blk = 0; blk < 4; ++blk) {
-        const int r_ = blk & 1, w_ = blk >> 1;
-        const int lo = r_ ? Sup::x1lo : Sup::x0lo;
-        const double *Xr = r_ ? X1 : X0;
-        const double *w = w_ ? a.pd : a.qd;
-        for (int e = hl; e < NRM; e += kHalf) {
-            const int ci = e % NU, cj = e / NU;
-            double acc = 0.0;
-#pragma unroll
-            for (int l = 0; l < SD; ++l) acc += Xr[ci * SD + l] * w[lo + l] * Xr[cj * SD + l];
-            S[e * 4 + blk] = acc;
-        }
-    }
-    // ---- u_m(c) = X0[:,c]' W_m e_m, v_m(c) = X1[:,c]' W_m e_m, m = 1..N
-    for (int e = hl; e < N * NU; e += kHalf) {
-        const int c = e % NU, m = 1 + e / NU;
-        const double md = (double)m, hm2 = 0.5 * md * md;
-        auto el = [&](int l) {
-            const double wl = (m < N) ? a.qd[l] : a.pd[l];
-            return wl * (x0g[l] + md * Ax[l] + hm2 * A2x[l] - xr[m * NX + l]);
+    if (work) {
+        // ---- model: lane i < NX holds row i of Ac; X0 = Bc Ts and X1 = (Ac Ts) X0 on their
+        //      support rows, A x0, A^2 x0 (A = Ac Ts).  Same products, in the same order, as the
+        //      one-QP kernel (the zero terms it adds are exact).
+        double Iwi[9];
+        double cy = 1.0, sy = 0.0;
+        if (MODEL == 0) srbm_rot_inertia(lin[0], a.Ibinv, cy, sy, Iwi);
+        auto entry = [&](int i, int j) -> double {  // [Ac | Bc](i, j)
+            return MODEL == 0 ? srbm_entry(i, j, lin, cy, sy, Iwi, a.mass)
+                              : literal_entry(i, j, lin, a.mass);
         };
-        double su = 0.0, sv = 0.0;
+        const double Ts = a.Ts;
+        double arow[NX];
 #pragma unroll
-        for (int l = Sup::x0lo; l < Sup::x0hi; ++l) su += X0[c * SD + l - Sup::x0lo] * el(l);
+        for (int k = 0; k < NX; ++k) arow[k] = entry(hl, k);
+        if (hl >= Sup::x0lo && hl < Sup::x0hi) {
 #pragma unroll
-        for (int l = Sup::x1lo; l < Sup::x1hi; ++l) sv += X1[c * SD + l - Sup::x1lo] * el(l);
-        UV[(m * 2 + 0) * NU + c] = su;
-        UV[(m * 2 + 1) * NU + c] = sv;
+            for (int c = 0; c < NU; ++c) X0[c * SD + hl - Sup::x0lo] = entry(hl, NX + c) * Ts;
+        }
+        if (hl < NX) {
+            double s = 0.0;
+#pragma unroll
+            for (int k = 0; k < NX; ++k) s += arow[k] * x0g[k];
+            Ax[hl] = s * Ts;
+        }
+        wave_sync();
+        if (hl >= Sup::x1lo && hl < Sup::x1hi) {
+#pragma unroll
+            for (int c = 0; c < NU; ++c) {
+                double s = 0.0;
+#pragma unroll
+                for (int k = Sup::x0lo; k < Sup::x0hi; ++k) s += arow[k] * X0[c * SD + k - Sup::x0lo];
+                X1[c * SD + hl - Sup::x1lo] = s * Ts;
+            }
+        }
+        if (hl < NX) {
+            double s = 0.0;
+#pragma unroll
+            for (int k = 0; k < NX; ++k) s += arow[k] * Ax[k];
+            A2x[hl] = s * Ts;
+        }
+        MPCQP_CUT(a.cut, 13);
+
+        // ---- S^W_rr = X_r' W X_r over the support rows (w: 0 = Q, 1 = P), entry o = cj NU + ci
+#pragma unroll
+        for (int blk = 0; blk < 4; ++blk) {
+            const int r_ = blk & 1, w_ = blk >> 1;
+            const int lo = r_ ? Sup::x1lo : Sup::x0lo;
+            const double *Xr = r_ ? X1 : X0;
+            const double *w = w_ ? a.pd : a.qd;
+            for (int e = hl; e < NRM; e += kHalf) {
+                const int ci = e % NU, cj = e / NU;
+                double acc = 0.0;
+#pragma unroll
+                for (int l = 0; l < SD; ++l) acc += Xr[ci * SD + l] * w[lo + l] * Xr[cj * SD + l];
+                S[e * 4 + blk] = acc;
+            }
+        }
+        // ---- u_m(c) = X0[:,c]' W_m e_m, v_m(c) = X1[:,c]' W_m e_m, m = 1..N
+        for (int e = hl; e < N * NU; e += kHalf) {
+            const int c = e % NU, m = 1 + e / NU;
+            const double md = (double)m, hm2 = 0.5 * md * md;
+            auto el = [&](int l) {
+                const double wl = (m < N) ? a.qd[l] : a.pd[l];
+                return wl * (x0g[l] + md * Ax[l] + hm2 * A2x[l] - xr[m * NX + l]);
+            };
+            double su = 0.0, sv = 0.0;
+#pragma unroll
+            for (int l = Sup::x0lo; l < Sup::x0hi; ++l) su += X0[c * SD + l - Sup::x0lo] * el(l);
+#pragma unroll
+            for (int l = Sup::x1lo; l < Sup::x1hi; ++l) sv += X1[c * SD + l - Sup::x1lo] * el(l);
+            UV[(m * 2 + 0) * NU + c] = su;
+            UV[(m * 2 + 1) * NU + c] = sv;
+        }
+        wave_sync();
     }
-    wave_sync();
+    MPCQP_STAMP(a.stamps, 1, tst);
     MPCQP_CUT(a.cut, 2);
 
     // ---- g (lane p: g_p), then H_FF over the dead early view (lane p loads row p)
@@ -413,10 +425,12 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         h[q] = in ? Hb[lrow(hl) + q] : ((q == hl) ? 1.0 : 0.0);
     }
     wave_sync();
+    MPCQP_STAMP(a.stamps, 3, tst);
     MPCQP_CUT(a.cut, 3);
 
     // ---- solver (gi_run_reg with NF = 30 per half)
-    double *Lc = D + Lay::oR, *R = D + Lay::oR;
+    constexpr bool kRinv = MPCQP_PAIR_RINV;
+    double *Lc = D + Lay::oR, *R = D + Lay::oR, *Ri = D + Lay::oR;  // R (or R^-1) over dead L
     double *rowbuf = D + Lay::oRow, *colb = rowbuf + NP, *rot = rowbuf + 2 * NP,
            *rinv = rowbuf + 4 * NP;
     double fval = 0.0, x = 0.0, u = 0.0;
@@ -509,6 +523,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         }
         if (ok && bad) status = ST_NOT_PD;
         ok2 = ok && status == ST_OK;
+        MPCQP_STAMP(a.stamps, 5, tst);
         MPCQP_CUT(a.cut, 4);
         MPCQP_CUT(a.cut, 5);
         // ---- unconstrained minimum x = -J t, objective -|t|^2 / 2
@@ -529,6 +544,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         fval = half_sum(hl < nf ? gv * gv : 0.0);
         fval = ok2 ? -0.5 * fval : 0.0;
     }
+    MPCQP_STAMP(a.stamps, 7, tst);
     MPCQP_CUT(a.cut, 6);
 
     // ---- dual active-set loop (Goldfarb-Idnani), flattened: one add or drop per pass, the
@@ -559,7 +575,14 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     bool done = !ok2;
     bool fresh = true;
     int p = 0;
+    MPCQP_SUB_INIT(tsub);
+#ifdef MPCQP_STAMPS
+    unsigned long long npass = 0;  // passes of this wavefront (diagnostic slot 2)
+#endif
     while (__ballot(!done) != 0ull) {
+#ifdef MPCQP_STAMPS
+        ++npass;
+#endif
         double dj = 0.0, sp = 0.0, z = 0.0, zn = 0.0, zq = 0.0, r = 0.0, t1 = INFINITY,
                t2 = INFINITY, t = 0.0, sg = 1.0, beta = 0.0;
         int kslot = 0x7fffffff, a_ = 0;
@@ -583,10 +606,23 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             wave_sync();
             dj = (hl < nf) ? sg * rowbuf[hl] : 0.0;
             sp = rowbuf[NP - 1];
+            if constexpr (kRinv) {
+                // r = R^-1 d(0:q): lane i < q takes row i of R^-1 (column-major packed, (i, j)
+                // at lrow(j) + i: consecutive lanes, consecutive addresses) against the
+                // published d (uniform address per half); independent products, no chain
+                const int qmax = max(__builtin_amdgcn_readlane(q, 0), __builtin_amdgcn_readlane(q, kHalf));
+                double r2[2] = {0.0, 0.0};
+                for (int j = 0; j < qmax; ++j) {
+                    const double rij = Ri[lrow(j) + hl], dv = rowbuf[j];
+                    r2[j & 1] += (hl <= j && j < q) ? rij * dv : 0.0;
+                }
+                r = (hl < q) ? sg * (r2[0] + r2[1]) : 0.0;
+            }
             if (hl < q) rowbuf[hl] = 0.0;  // after every lane's read (LDS keeps program order)
             wave_sync();
             if (iters >= max_iter) { status = ST_ITER_LIMIT; done = true; }
         }
+        MPCQP_SUB(tsub, 0);
         const bool stepping = go && !done;
         if (stepping) {
             ++iters;
@@ -602,15 +638,17 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             }
             z = sg * ((z4[0] + z4[1]) + (z4[2] + z4[3]));
             pin(z);  // here, not sunk to its use after the R solve: the row would stay live
-            // r = R^-1 d(0:q): uniform loop to the larger q of the two halves
-            const int qmax = max(__builtin_amdgcn_readlane(q, 0), __builtin_amdgcn_readlane(q, kHalf));
             if (q > 0) {
-                double val = dj;
-                for (int j = qmax - 1; j >= 0; --j) {
-                    const double rj = hread_rt(val, j) * rinv[j];
-                    if (j < q) {
-                        if (hl == j) r = rj;
-                        if (hl < j) val -= R[roff(j) + hl] * rj;
+                if constexpr (!kRinv) {
+                    // r = R^-1 d(0:q): uniform loop to the larger q of the two halves
+                    const int qmax = max(__builtin_amdgcn_readlane(q, 0), __builtin_amdgcn_readlane(q, kHalf));
+                    double val = dj;
+                    for (int j = qmax - 1; j >= 0; --j) {
+                        const double rj = hread_rt(val, j) * rinv[j];
+                        if (j < q) {
+                            if (hl == j) r = rj;
+                            if (hl < j) val -= R[roff(j) + hl] * rj;
+                        }
                     }
                 }
                 const double rmax = half_max(hl < q ? fabs(r) : 0.0);
@@ -622,6 +660,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             t = t1 < t2 ? t1 : t2;
             if (isinf(t)) { status = ST_INFEASIBLE; done = true; }
         }
+        MPCQP_SUB(tsub, 1);
         const bool moving = stepping && !done;
         bool add = false;
         if (moving) {
@@ -646,8 +685,16 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 }
                 wave_sync();
                 if (hl == q) rowbuf[q] = sg * vq;
-                if (hl < q) R[roff(q) + hl] = dj;
-                if (hl == q) { R[roff(q) + q] = rqq; rinv[q] = 1.0 / rqq; act = p; }
+                if constexpr (kRinv) {
+                    // R^-1 of [[R, d1], [0, rqq]] = [[R^-1, -R^-1 d1 / rqq], [0, 1 / rqq]], and
+                    // R^-1 d1 is this pass's r
+                    const double irq = 1.0 / rqq;
+                    if (hl < q) Ri[lrow(q) + hl] = -r * irq;
+                    if (hl == q) { Ri[lrow(q) + q] = irq; act = p; }
+                } else {
+                    if (hl < q) R[roff(q) + hl] = dj;
+                    if (hl == q) { R[roff(q) + q] = rqq; rinv[q] = 1.0 / rqq; act = p; }
+                }
                 if (hl == a_) stb &= lower ? ~1 : ~2;
                 ++q;
                 fresh = true;
@@ -664,46 +711,86 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                     const int an = __shfl(act, src, kWave);
                     if (hl >= k && hl < q) { u = un; act = an; }
                 }
-                for (int j = k; j < q - 1; ++j) {
-                    const double v = (hl <= j + 1) ? R[roff(j + 1) + hl] : 0.0;
+                if constexpr (kRinv) {
+                    // Removing column k of R and restoring the triangle with Givens G on rows
+                    // (j, j+1), j = k .. q-2, is, for R^-1, R^-1 G' with row k then deleted and the
+                    // last column dropped, where the same rotations zero row k of R^-1 G' left of
+                    // column q-1 (row k of (G R)^-1 is a multiple of e_{q-1}').  So the rotations
+                    // come from row k of R^-1 alone: every lane of the half runs the same chain
+                    // a <- hypot(a, R^-1(k, j+1)) on broadcast reads; (c, s) go to LDS for J.
+                    double ra = Ri[lrow(k) + k];
+                    rot[2 * hl] = 1.0;
+                    rot[2 * hl + 1] = 0.0;
                     wave_sync();
-                    if (hl <= j + 1) R[roff(j) + hl] = v;
-                    wave_sync();
-                }
-                --q;
-                rot[2 * hl] = 1.0;
-                rot[2 * hl + 1] = 0.0;
-                wave_sync();
-                for (int j = k; j < q; ++j) {
-                    const double aa = R[roff(j) + j], bb = R[roff(j) + j + 1];
-                    if (bb != 0.0) {
-                        const double hh = sqrt(aa * aa + bb * bb);
-                        const double ih = 1.0 / hh;
-                        const double c = aa * ih, s_ = bb * ih;
-                        const int l = j + 1 + hl;
-                        double r0 = 0.0, r1 = 0.0;
-                        if (l < q) { r0 = R[roff(l) + j]; r1 = R[roff(l) + j + 1]; }
-                        wave_sync();
-                        if (l < q) {
-                            R[roff(l) + j] = c * r0 + s_ * r1;
-                            R[roff(l) + j + 1] = -s_ * r0 + c * r1;
+                    for (int j = k; j < q - 1; ++j) {
+                        const double rb = Ri[lrow(j + 1) + k];
+                        double c = 1.0, s_ = 0.0;
+                        if (ra != 0.0) {
+                            const double hh = sqrt(ra * ra + rb * rb), ih = 1.0 / hh;
+                            c = rb * ih;
+                            s_ = -ra * ih;
+                            ra = hh;
+                        } else {
+                            ra = rb;
                         }
+                        // lane i's entries (i, j), (i, j+1) of R^-1 G' (rows i <= j+1 are
+                        // nonzero); rotated column j is final: it is written with row k deleted
+                        // (rows below k move up one, so it fits its j+1 packed slots again),
+                        // column j+1 goes back in place for the next rotation
+                        const double y0 = (hl <= j) ? Ri[lrow(j) + hl] : 0.0;
+                        const double y1 = (hl <= j + 1) ? Ri[lrow(j + 1) + hl] : 0.0;
                         if (hl == 0) {
-                            R[roff(j) + j] = hh;
-                            R[roff(j) + j + 1] = 0.0;
-                            rinv[j] = ih;
                             rot[2 * j] = c;
                             rot[2 * j + 1] = s_;
                         }
+                        if (hl <= j + 1 && hl != k) Ri[lrow(j) + hl - (hl > k ? 1 : 0)] = c * y0 + s_ * y1;
+                        if (hl <= j + 1) Ri[lrow(j + 1) + hl] = -s_ * y0 + c * y1;
                         wave_sync();
-                    } else {
-                        if (hl == 0) rinv[j] = 1.0 / aa;
+                    }
+                    --q;
+                } else {
+                    for (int j = k; j < q - 1; ++j) {
+                        const double v = (hl <= j + 1) ? R[roff(j + 1) + hl] : 0.0;
                         wave_sync();
+                        if (hl <= j + 1) R[roff(j) + hl] = v;
+                        wave_sync();
+                    }
+                    --q;
+                    rot[2 * hl] = 1.0;
+                    rot[2 * hl + 1] = 0.0;
+                    wave_sync();
+                    for (int j = k; j < q; ++j) {
+                        const double aa = R[roff(j) + j], bb = R[roff(j) + j + 1];
+                        if (bb != 0.0) {
+                            const double hh = sqrt(aa * aa + bb * bb);
+                            const double ih = 1.0 / hh;
+                            const double c = aa * ih, s_ = bb * ih;
+                            const int l = j + 1 + hl;
+                            double r0 = 0.0, r1 = 0.0;
+                            if (l < q) { r0 = R[roff(l) + j]; r1 = R[roff(l) + j + 1]; }
+                            wave_sync();
+                            if (l < q) {
+                                R[roff(l) + j] = c * r0 + s_ * r1;
+                                R[roff(l) + j + 1] = -s_ * r0 + c * r1;
+                            }
+                            if (hl == 0) {
+                                R[roff(j) + j] = hh;
+                                R[roff(j) + j + 1] = 0.0;
+                                rinv[j] = ih;
+                                rot[2 * j] = c;
+                                rot[2 * j + 1] = s_;
+                            }
+                            wave_sync();
+                        } else {
+                            if (hl == 0) rinv[j] = 1.0 / aa;
+                            wave_sync();
+                        }
                     }
                 }
             }
         }
         wave_sync();
+        MPCQP_SUB(tsub, 2);
         if (!done && fresh) {
             // ---- most violated inactive bound (lowest id on ties): before the first step and
             //      right after every add, so a half's last add also ends its solve (no checking
@@ -765,15 +852,24 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             }
         }
         wave_sync();
+        MPCQP_SUB(tsub, 3);
     }
+    MPCQP_SUB_FLUSH(a.stamps, tsub);
+#ifdef MPCQP_STAMPS
+    if (a.stamps && ln == 0) atomicAdd(&a.stamps[2], npass);
+#endif
 
+    MPCQP_STAMP(a.stamps, 8, tst);
     MPCQP_CUT(a.cut, 7);
     // ---- outputs
     const int bo = (int)(long long)ctl[1];
     const bool defer = a.ovf && nf > NF && nf <= a.max_free;  // the workgroup kernel takes it
-    if (bo >= 0 && defer) {
-        if (hl == 0) wg_list_append(a.ovf, bo);
-    } else if (bo >= 0) {
+    {  // one append (one atomic) for the wavefront's deferred instances
+        const int b0 = __builtin_amdgcn_readlane(bo, 0), b1 = __builtin_amdgcn_readlane(bo, kHalf);
+        const uint64_t dm = __ballot(defer && bo >= 0);
+        if (dm && ln == 0) wg_list_append(a.ovf, a.ovf_cap, b0, dm & 1ull, b1, (dm >> kHalf) & 1ull);
+    }
+    if (bo >= 0 && !defer) {
         // U assembled in LDS (the dead L / R space), then written once, coalesced: a
         // non-temporal store of a partial line is its own HBM write
         const uint64_t cto = *ctl;
@@ -809,6 +905,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         sel_commit(a, k0 < k1 ? k0 : k1, NV, true,
                    reinterpret_cast<unsigned long long *>(smem) + Lay::oR);
     }
+    MPCQP_STAMP(a.stamps, 9, tst);
     (void)NS;
 }
 

@@ -9,7 +9,8 @@
 // takes the dense nV = NU*N problem whatever the bound pattern (src/QPSolver.cpp:87-96).
 //
 // Routing: the one-wave kernels (k_mpc_pair, k_mpc) append an instance whose free-variable
-// count exceeds their register capacity to the context's overflow list (atomic counter) and
+// count exceeds their register capacity to the context's overflow list (64 sub-lists, one
+// atomic per deferring wavefront, mpc_fused.hpp) and
 // leave its outputs alone; k_mpc_wg, launched right after on the same stream with a resident
 // grid, solves the listed instances and writes their outputs; the last workgroup to finish
 // re-arms the list.  An empty list costs one short launch.
@@ -157,11 +158,13 @@ __device__ __forceinline__ void wg_mpc_grid(const MpcArgs &a, int *list, int *re
         }
         return;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0)
-        __hip_atomic_store(rearm, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int count = __hip_atomic_load(&list[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0 && threadIdx.x < kListSubs)
+        __hip_atomic_store(&rearm[threadIdx.x * kListStride], 0, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    const OvfView ov = ovf_view(list, a.ovf_cap);
+    const int count = ov.total;
     for (int i = blockIdx.x; i < count; i += gridDim.x) {
-        wg_mpc_one<NU, N, MODEL, FRIC, GEN, NF>(a, list[kListHead + i], smem);
+        wg_mpc_one<NU, N, MODEL, FRIC, GEN, NF>(a, ov.id(i), smem);
         __syncthreads();
     }
     if (a.sel) {
@@ -169,12 +172,11 @@ __device__ __forceinline__ void wg_mpc_grid(const MpcArgs &a, int *list, int *re
         // back the keys of the block's instances (its own stores, gi_write_wg) once the solves
         // are done; the solves' LDS is dead, the finalizer's scratch
         unsigned long long kmin = kSelNone;
-        if (threadIdx.x == 0)
-            for (int i = blockIdx.x; i < count; i += gridDim.x) {
-                const int b = list[kListHead + i];
-                const unsigned long long k = sel_key(a.status[b], a.cost[b], a.sel_base + b);
-                kmin = k < kmin ? k : kmin;
-            }
+        for (int i = blockIdx.x; i < count; i += gridDim.x) {
+            const int b = ov.id(i);
+            const unsigned long long k = sel_key(a.status[b], a.cost[b], a.sel_base + b);
+            kmin = k < kmin ? k : kmin;
+        }
         sel_commit(a, kmin, NU * N, (int)blockIdx.x < count,
                    reinterpret_cast<unsigned long long *>(smem));
     }

@@ -517,9 +517,13 @@ struct mpcqp_ctx {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     bool timing = false;
-    hipEvent_t ev[6];
+    // timing (mpcqp_enable_timing): per slot a ring of begin / end event pairs, the last
+    // kTimingRing launches since the last mpcqp_kernel_ms_sum (created on first enable)
+    static constexpr int kTimingRing = 64;
+    hipEvent_t ev[4][kTimingRing][2];
     bool ev_ok = false;
-    bool ev_used[3] = {false, false, false};
+    int ev_n[4] = {0, 0, 0, 0};       // launches recorded since the last sum
+    long long ev_seq[4] = {0, 0, 0, 0};  // launches recorded in total (ring position)
     double *scratchH = nullptr, *scratchF = nullptr;
     size_t scratch_cap = 0;
     // fast path
@@ -534,9 +538,19 @@ struct mpcqp_ctx {
     size_t list_cap = 0;                    // instances a list holds
     int list_par = 0;                       // the list the next launch fills
     int wg_grid = 0;                        // resident workgroups of the workgroup kernel
-    // host-pointer entry point staging
+    // host-pointer entry point (mpcqp_batch_solve_host): device staging, pinned host staging of
+    // the same byte layout (one copy each way), its own stream (graph capture needs one) and
+    // the instantiated graphs of the last batch size (one per overflow-list parity)
     void *hbuf = nullptr;
     size_t hbuf_cap = 0;
+    void *pin = nullptr;
+    size_t pin_cap = 0;
+    hipStream_t hstream = nullptr;
+    hipEvent_t hev = nullptr;
+    int hg_B = 0;
+    bool hg_ovf = false;
+    hipGraphExec_t hg_exec[2] = {nullptr, nullptr};
+    bool hg_off = false;  // capture failed once: run the host path uncaptured
     // closed-loop rollout workspace
     void *rbuf = nullptr;
     size_t rbuf_cap = 0;
@@ -849,9 +863,6 @@ int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
         c->wg_grid = std::max(1, nb) * std::max(1, dev_cus);
     }
     c->m.Q = c->m.R = c->m.P = nullptr;  // host pointers are not kept
-    c->ev_ok = true;
-    for (int i = 0; i < 6; ++i)
-        if (hipEventCreate(&c->ev[i]) != hipSuccess) c->ev_ok = false;
     *out = c;
     return MPCQP_OK;
 }
@@ -900,13 +911,20 @@ int mpcqp_ctx_destroy(mpcqp_ctx *c) {
     hipFree(c->dsel);
     hipFree(c->dlist);
     hipFree(c->hbuf);
+    for (int i = 0; i < 2; ++i)
+        if (c->hg_exec[i]) hipGraphExecDestroy(c->hg_exec[i]);
+    if (c->pin) hipHostFree(c->pin);
+    if (c->hev) hipEventDestroy(c->hev);
+    if (c->hstream) hipStreamDestroy(c->hstream);
     hipFree(c->rbuf);
     hipFree(c->fkbuf);
     hipFree(c->dwarm);
     hipFree(c->scratchH);
     hipFree(c->scratchF);
     if (c->ev_ok)
-        for (int i = 0; i < 6; ++i) hipEventDestroy(c->ev[i]);
+        for (int w = 0; w < 4; ++w)
+            for (int i = 0; i < mpcqp_ctx::kTimingRing; ++i)
+                for (int e = 0; e < 2; ++e) hipEventDestroy(c->ev[w][i][e]);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     delete c;
     return MPCQP_OK;
@@ -930,23 +948,58 @@ int mpcqp_sync(mpcqp_ctx *c) {
 
 int mpcqp_enable_timing(mpcqp_ctx *c, int on) {
     if (!c) return MPCQP_ERR_BAD_ARG;
+    if (on && !c->ev_ok) {
+        hipSetDevice(c->device);
+        bool ok = true;
+        for (int w = 0; w < 4; ++w)
+            for (int i = 0; i < mpcqp_ctx::kTimingRing; ++i)
+                for (int e = 0; e < 2; ++e)
+                    if (hipEventCreate(&c->ev[w][i][e]) != hipSuccess) ok = false;
+        if (!ok) return MPCQP_ERR_DEVICE;
+        c->ev_ok = true;
+    }
     c->timing = on && c->ev_ok;
     return MPCQP_OK;
 }
 
-double mpcqp_last_kernel_ms(mpcqp_ctx *c, int which) {
-    if (!c || which < 0 || which > 2 || !c->ev_used[which]) return -1.0;
+static double ev_ms(mpcqp_ctx *c, int which, long long seq) {
+    hipEvent_t *p = c->ev[which][seq % mpcqp_ctx::kTimingRing];
     float ms = -1.0f;
-    if (hipEventSynchronize(c->ev[2 * which + 1]) != hipSuccess) return -1.0;
-    if (hipEventElapsedTime(&ms, c->ev[2 * which], c->ev[2 * which + 1]) != hipSuccess) return -1.0;
+    if (hipEventSynchronize(p[1]) != hipSuccess) return -1.0;
+    if (hipEventElapsedTime(&ms, p[0], p[1]) != hipSuccess) return -1.0;
     return ms;
 }
 
+double mpcqp_last_kernel_ms(mpcqp_ctx *c, int which) {
+    if (!c || which < 0 || which > 3 || !c->ev_ok || c->ev_seq[which] == 0) return -1.0;
+    return ev_ms(c, which, c->ev_seq[which] - 1);
+}
+
+double mpcqp_kernel_ms_sum(mpcqp_ctx *c, int which, int *count) {
+    if (count) *count = 0;
+    if (!c || which < 0 || which > 3 || !c->ev_ok) return -1.0;
+    const int n = std::min(c->ev_n[which], mpcqp_ctx::kTimingRing);
+    double sum = 0.0;
+    for (int i = 0; i < n; ++i) {
+        const double ms = ev_ms(c, which, c->ev_seq[which] - 1 - i);
+        if (ms < 0.0) return -1.0;
+        sum += ms;
+    }
+    c->ev_n[which] = 0;
+    if (count) *count = n;
+    return sum;
+}
+
 static void tbegin(mpcqp_ctx *c, int which) {
-    if (c->timing) hipEventRecord(c->ev[2 * which], c->stream);
+    if (c->timing)
+        hipEventRecord(c->ev[which][c->ev_seq[which] % mpcqp_ctx::kTimingRing][0], c->stream);
 }
 static void tend(mpcqp_ctx *c, int which) {
-    if (c->timing) { hipEventRecord(c->ev[2 * which + 1], c->stream); c->ev_used[which] = true; }
+    if (c->timing) {
+        hipEventRecord(c->ev[which][c->ev_seq[which] % mpcqp_ctx::kTimingRing][1], c->stream);
+        ++c->ev_seq[which];
+        ++c->ev_n[which];
+    }
 }
 
 static CondenseArgs batch_condense_args(mpcqp_ctx *c, int B, const double *x0, const double *xref,
@@ -1065,17 +1118,19 @@ static int ensure_warm(mpcqp_ctx *c, int B) {
     return MPCQP_OK;
 }
 
-// overflow list for B instances (grown on demand; mpcqp_ctx_reserve sizes it up front)
+// overflow list for B instances (grown on demand; mpcqp_ctx_reserve sizes it up front): two
+// lists (alternate launches), each kListSubs counters then kListSubs sub-lists (mpc_fused.hpp)
+static size_t list_stride(size_t cap) { return kListHeadWords + kListSubs * (size_t)ovf_list_cap((long long)cap); }
 static int ensure_list(mpcqp_ctx *c, int B) {
     if (c->list_cap >= (size_t)B) return MPCQP_OK;
     if (c->dlist) hipStreamSynchronize(c->stream);
     hipFree(c->dlist);
     c->dlist = nullptr;
     c->list_cap = 0;
-    const size_t stride = kListHead + (size_t)B;
+    const size_t stride = list_stride((size_t)B);
     if (hipMalloc(&c->dlist, sizeof(int) * 2 * stride) != hipSuccess ||
-        hipMemsetAsync(c->dlist, 0, sizeof(int) * kListHead, c->stream) != hipSuccess ||
-        hipMemsetAsync(c->dlist + stride, 0, sizeof(int) * kListHead, c->stream) != hipSuccess)
+        hipMemsetAsync(c->dlist, 0, sizeof(int) * kListHeadWords, c->stream) != hipSuccess ||
+        hipMemsetAsync(c->dlist + stride, 0, sizeof(int) * kListHeadWords, c->stream) != hipSuccess)
         return MPCQP_ERR_DEVICE;
     c->list_cap = B;
     c->list_par = 0;
@@ -1085,27 +1140,32 @@ static int ensure_list(mpcqp_ctx *c, int B) {
 // the fused step: two instances per wave when the paired kernel is instantiated; instances
 // beyond the one-wave kernel's free capacity go through the overflow list to the workgroup
 // kernel, launched right after on the same stream
-static int launch_mpc(mpcqp_ctx *c, bool gen, int B, MpcArgs *a) {
+static int launch_mpc(mpcqp_ctx *c, bool gen, int B, MpcArgs *a, bool may_overflow = true) {
     a->ovf = nullptr;
     int *list = nullptr, *rearm = nullptr;
-    if (c->fk.wg && !gen) {
+    if (c->fk.wg && !gen && may_overflow) {
         const int rc = ensure_list(c, B);
         if (rc) return rc;
-        const size_t stride = kListHead + c->list_cap;
+        const size_t stride = list_stride(c->list_cap);
         list = c->dlist + (c->list_par ? stride : 0);
         rearm = c->dlist + (c->list_par ? 0 : stride);
         a->ovf = list;
+        a->ovf_cap = ovf_list_cap((long long)c->list_cap);
     }
     const void *pk = gen ? c->fk.pair_gen : c->fk.pair;
     a->sel_final = a->ovf ? 0 : 1;  // fused selection: the batch's last launch finalizes
+    tbegin(c, 2);
     int rc = pk ? launch(pk, (B + 1) / 2, c->fk.pair_lds, c->stream, a)
                 : launch(gen ? c->fk.mpc_gen : c->fk.mpc, B, c->fk.mpc_lds, c->stream, a);
+    tend(c, 2);
     if (rc || !a->ovf) return rc;
     a->sel_final = 1;
     void *args[] = {a, &list, &rearm};
     const int grid = std::max(1, std::min(B, c->wg_grid));
+    tbegin(c, 3);
     rc = hip_status(hipLaunchKernel(c->fk.wg, dim3(grid), dim3(c->fk.wg_threads), args, c->fk.wg_lds,
                                     c->stream));
+    tend(c, 3);
     c->list_par ^= 1;
     return rc;
 }
@@ -1248,9 +1308,19 @@ int mpcqp_batch_condense_solve(mpcqp_ctx *c, int B, const double *AB, const doub
     return mpcqp_batch_solve_qp(c, B, c->scratchH, c->scratchF, contact, U, cost, status, iters);
 }
 
+static int batch_solve(mpcqp_ctx *c, int B, const double *x0, const double *xref,
+                       const double *lin, const uint64_t *contact, double *U, double *cost,
+                       int *status, int *iters, bool may_overflow);
+
 int mpcqp_batch_solve(mpcqp_ctx *c, int B, const double *x0, const double *xref,
                       const double *lin, const uint64_t *contact, double *U, double *cost,
                       int *status, int *iters) {
+    return batch_solve(c, B, x0, xref, lin, contact, U, cost, status, iters, true);
+}
+
+static int batch_solve(mpcqp_ctx *c, int B, const double *x0, const double *xref,
+                       const double *lin, const uint64_t *contact, double *U, double *cost,
+                       int *status, int *iters, bool may_overflow) {
     if (!c) return MPCQP_ERR_BAD_ARG;
     if (B <= 0) return B == 0 ? MPCQP_OK : MPCQP_ERR_BAD_ARG;
     hipSetDevice(c->device);
@@ -1273,7 +1343,7 @@ int mpcqp_batch_solve(mpcqp_ctx *c, int B, const double *x0, const double *xref,
             rc = hip_status(hipLaunchKernel(c->fk.dense, dim3(B), dim3(c->fk.dense_threads), args,
                                             c->fk.dense_lds, c->stream));
         } else {
-            rc = launch_mpc(c, false, B, &a);
+            rc = launch_mpc(c, false, B, &a, may_overflow);
         }
         tend(c, 1);
         return rc;
@@ -1357,6 +1427,51 @@ int mpcqp_ctx_fk_feet_host(mpcqp_ctx *c, int R, const double *q, const double *r
     return hip_status(hipStreamSynchronize(c->stream));
 }
 
+// Can an instance of this host batch need more free variables than the one-wave kernel holds
+// (so the overflow workgroup kernel must run)?  The free count follows from the contact word
+// alone: the forces of a foot in contact are free, a swing foot's are fixed (SRBM); every input
+// is free in the literal model.
+static bool host_may_overflow(const mpcqp_ctx *c, int B, const uint64_t *contact) {
+    if (!c->fast || !c->fk.wg) return false;
+    if (c->m.model != MPCQP_MODEL_SRBM || !contact) return true;
+    const int N = c->m.N;
+    const uint64_t mask = N >= 32 ? ~0ull : ((1ull << (2 * N)) - 1ull);
+    for (int i = 0; i < B; ++i)
+        if (3 * __builtin_popcountll(contact[i] & mask) > c->fk.prim_nf) return true;
+    return false;
+}
+
+// the host path's step on its staging, as the stream work of one call: H2D of the inputs, the
+// solve, D2H of the outputs (captured once into a graph per batch size and list parity)
+static int host_step(mpcqp_ctx *c, int B, bool ovf, size_t in_bytes, size_t out_off,
+                     size_t out_bytes, bool has_contact) {
+    const size_t nx = c->m.nx, N = c->m.N, nV = (size_t)c->m.nu * c->m.N;
+    const size_t lin_w = c->m.model == MPCQP_MODEL_DENSE ? nx * (nx + c->m.nu) : 8;
+    char *d = (char *)c->hbuf;
+    double *d_x0 = (double *)d, *d_xr = d_x0 + nx * B, *d_lin = d_xr + nx * (N + 1) * B;
+    uint64_t *d_ct = (uint64_t *)(d_lin + lin_w * B);
+    double *d_U = (double *)(d + out_off), *d_cost = d_U + nV * B;
+    int *d_st = (int *)(d_cost + B), *d_it = d_st + B;
+    if (hipMemcpyAsync(d, c->pin, in_bytes, hipMemcpyHostToDevice, c->hstream) != hipSuccess)
+        return MPCQP_ERR_DEVICE;
+    hipStream_t keep = c->stream;
+    c->stream = c->hstream;
+    const int rc = batch_solve(c, B, d_x0, d_xr, d_lin, has_contact ? d_ct : nullptr, d_U, d_cost,
+                               d_st, d_it, ovf);
+    c->stream = keep;
+    if (rc) return rc;
+    if (hipMemcpyAsync((char *)c->pin + out_off, d + out_off, out_bytes, hipMemcpyDeviceToHost,
+                       c->hstream) != hipSuccess)
+        return MPCQP_ERR_DEVICE;
+    return MPCQP_OK;
+}
+
+static void host_graphs_drop(mpcqp_ctx *c) {
+    for (int i = 0; i < 2; ++i)
+        if (c->hg_exec[i]) { hipGraphExecDestroy(c->hg_exec[i]); c->hg_exec[i] = nullptr; }
+    c->hg_B = 0;
+}
+
 int mpcqp_batch_solve_host(mpcqp_ctx *c, int B, const double *x0, const double *xref,
                            const double *lin, const uint64_t *contact, double *U, double *cost,
                            int *status, int *iters) {
@@ -1365,29 +1480,89 @@ int mpcqp_batch_solve_host(mpcqp_ctx *c, int B, const double *x0, const double *
     if (c->m.model == MPCQP_MODEL_SRBM && !contact) return MPCQP_ERR_BAD_ARG;
     if (B == 0) return MPCQP_OK;
     hipSetDevice(c->device);
+    // one byte layout on both sides: inputs [x0 | xref | lin | contact], then (16-B aligned)
+    // outputs [U | cost | status | iters]
     const size_t nx = c->m.nx, N = c->m.N, nV = (size_t)c->m.nu * c->m.N;
     const size_t lin_w = c->m.model == MPCQP_MODEL_DENSE ? nx * (nx + c->m.nu) : 8;
-    const size_t n_x0 = nx * B, n_xr = nx * (N + 1) * B, n_lin = lin_w * B, n_u = nV * B;
-    if (ensure_bytes(c, &c->hbuf, &c->hbuf_cap, host_stage_bytes(c, B))) return MPCQP_ERR_DEVICE;
-    double *d_x0 = (double *)c->hbuf, *d_xr = d_x0 + n_x0, *d_lin = d_xr + n_xr,
-           *d_U = d_lin + n_lin, *d_cost = d_U + n_u;
-    uint64_t *d_ct = (uint64_t *)(d_cost + B);
-    int *d_st = (int *)(d_ct + B), *d_it = d_st + B;
-    const hipMemcpyKind h2d = hipMemcpyHostToDevice, d2h = hipMemcpyDeviceToHost;
-    if (hipMemcpyAsync(d_x0, x0, sizeof(double) * n_x0, h2d, c->stream) != hipSuccess ||
-        hipMemcpyAsync(d_xr, xref, sizeof(double) * n_xr, h2d, c->stream) != hipSuccess ||
-        hipMemcpyAsync(d_lin, lin, sizeof(double) * n_lin, h2d, c->stream) != hipSuccess ||
-        (contact && hipMemcpyAsync(d_ct, contact, sizeof(uint64_t) * B, h2d, c->stream) != hipSuccess))
+    const size_t b_x0 = sizeof(double) * nx * B, b_xr = sizeof(double) * nx * (N + 1) * B,
+                 b_lin = sizeof(double) * lin_w * B, b_ct = contact ? sizeof(uint64_t) * B : 0;
+    const size_t in_bytes = b_x0 + b_xr + b_lin + sizeof(uint64_t) * B;
+    const size_t out_off = (in_bytes + 15) & ~(size_t)15;
+    const size_t b_u = sizeof(double) * nV * B, b_c = sizeof(double) * B, b_i = sizeof(int) * B;
+    const size_t out_bytes = b_u + b_c + 2 * b_i, total = out_off + out_bytes;
+    const void *hb = c->hbuf;
+    if (ensure_bytes(c, &c->hbuf, &c->hbuf_cap, std::max(total, host_stage_bytes(c, B))))
         return MPCQP_ERR_DEVICE;
-    int rc = mpcqp_batch_solve(c, B, d_x0, d_xr, d_lin, contact ? d_ct : nullptr, d_U, d_cost,
-                               d_st, d_it);
+    if (c->pin_cap < total) {
+        if (c->pin) hipHostFree(c->pin);
+        c->pin = nullptr;
+        c->pin_cap = 0;
+        if (hipHostMalloc(&c->pin, total, hipHostMallocDefault) != hipSuccess) return MPCQP_ERR_DEVICE;
+        c->pin_cap = total;
+        host_graphs_drop(c);
+    }
+    if (c->hbuf != hb) host_graphs_drop(c);
+    if (!c->hstream) {
+        if (hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&c->hev, hipEventDisableTiming) != hipSuccess)
+            return MPCQP_ERR_DEVICE;
+    }
+    const bool ovf = host_may_overflow(c, B, contact);
+    if (ovf && ensure_list(c, B)) return MPCQP_ERR_DEVICE;  // (allocates outside any capture)
+    char *h = (char *)c->pin;
+    memcpy(h, x0, b_x0);
+    memcpy(h + b_x0, xref, b_xr);
+    memcpy(h + b_x0 + b_xr, lin, b_lin);
+    if (b_ct) memcpy(h + b_x0 + b_xr + b_lin, contact, b_ct);
+    // after the context's earlier work (the overflow lists, buffers it may still use)
+    if (hipEventRecord(c->hev, c->stream) != hipSuccess ||
+        hipStreamWaitEvent(c->hstream, c->hev, 0) != hipSuccess)
+        return MPCQP_ERR_DEVICE;
+    int rc = MPCQP_OK;
+    const bool graph = c->fast && !c->hg_off;
+    if (graph) {
+        if (c->hg_B != B || c->hg_ovf != ovf) {
+            host_graphs_drop(c);
+            c->hg_B = B;
+            c->hg_ovf = ovf;
+        }
+        const int par = ovf ? c->list_par : 0;
+        if (!c->hg_exec[par]) {
+            // capture one call's stream work; the capture does not run it, so the list parity
+            // the capture advanced is put back (the launch below advances it)
+            const bool timing = c->timing;
+            c->timing = false;
+            hipGraph_t g = nullptr;
+            bool ok = hipStreamBeginCapture(c->hstream, hipStreamCaptureModeThreadLocal) == hipSuccess;
+            const int rcc = ok ? host_step(c, B, ovf, in_bytes, out_off, out_bytes, b_ct != 0) : MPCQP_OK;
+            if (ok) ok = hipStreamEndCapture(c->hstream, &g) == hipSuccess && rcc == MPCQP_OK;
+            c->list_par = ovf ? par : c->list_par;
+            c->timing = timing;
+            if (ok) ok = hipGraphInstantiate(&c->hg_exec[par], g, nullptr, nullptr, 0) == hipSuccess;
+            if (g) hipGraphDestroy(g);
+            if (!ok) {
+                c->hg_exec[par] = nullptr;
+                c->hg_off = true;  // fall back to direct launches from now on
+                (void)hipGetLastError();
+            }
+        }
+        if (c->hg_exec[par]) {
+            if (hipGraphLaunch(c->hg_exec[par], c->hstream) != hipSuccess) return MPCQP_ERR_DEVICE;
+            if (ovf) c->list_par ^= 1;
+        } else {
+            rc = host_step(c, B, ovf, in_bytes, out_off, out_bytes, b_ct != 0);
+        }
+    } else {
+        rc = host_step(c, B, ovf, in_bytes, out_off, out_bytes, b_ct != 0);
+    }
     if (rc) return rc;
-    if (hipMemcpyAsync(U, d_U, sizeof(double) * n_u, d2h, c->stream) != hipSuccess ||
-        hipMemcpyAsync(cost, d_cost, sizeof(double) * B, d2h, c->stream) != hipSuccess ||
-        hipMemcpyAsync(status, d_st, sizeof(int) * B, d2h, c->stream) != hipSuccess ||
-        hipMemcpyAsync(iters, d_it, sizeof(int) * B, d2h, c->stream) != hipSuccess)
-        return MPCQP_ERR_DEVICE;
-    return hip_status(hipStreamSynchronize(c->stream));
+    rc = hip_status(hipStreamSynchronize(c->hstream));
+    if (rc) return rc;
+    memcpy(U, h + out_off, b_u);
+    memcpy(cost, h + out_off + b_u, b_c);
+    memcpy(status, h + out_off + b_u + b_c, b_i);
+    memcpy(iters, h + out_off + b_u + b_c + b_i, b_i);
+    return MPCQP_OK;
 }
 
 int mpcqp_set_warm_start(mpcqp_ctx *c, int on) {

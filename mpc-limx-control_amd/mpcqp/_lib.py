@@ -28,7 +28,7 @@ EXPORTS = [
     "mpcqp_debug_phase_cycles", "mpcqp_batch_solve_host",
     "mpcqp_batch_select_min", "mpcqp_batch_select_record", "mpcqp_reduce_records",
     "mpcqp_batch_solve_select",
-    "mpcqp_enable_timing", "mpcqp_last_kernel_ms",
+    "mpcqp_enable_timing", "mpcqp_last_kernel_ms", "mpcqp_kernel_ms_sum",
     "mpcqp_batch_solve_gait", "mpcqp_batch_select_state", "mpcqp_batch_plant_srbm",
     "mpcqp_rollout", "mpcqp_fk_feet", "mpcqp_kf_update", "mpcqp_ctx_reserve",
     "mpcqp_ctx_fk_feet_host", "mpcqp_set_warm_start",
@@ -100,6 +100,8 @@ def lib():
     L.mpcqp_enable_timing.argtypes = [vp, i]
     L.mpcqp_last_kernel_ms.argtypes = [vp, i]
     L.mpcqp_last_kernel_ms.restype = C.c_double
+    L.mpcqp_kernel_ms_sum.argtypes = [vp, i, C.POINTER(C.c_int)]
+    L.mpcqp_kernel_ms_sum.restype = C.c_double
     L.mpcqp_status_string.argtypes = [i]
     L.mpcqp_status_string.restype = C.c_char_p
     L.mpcqp_device_count.argtypes = []

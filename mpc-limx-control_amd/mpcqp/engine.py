@@ -204,10 +204,18 @@ class BatchEngine:
         check("mpcqp_sync", lib().mpcqp_sync(self.ctx))
 
     def enable_timing(self, on=True):
-        lib().mpcqp_enable_timing(self.ctx, 1 if on else 0)
+        check("mpcqp_enable_timing", lib().mpcqp_enable_timing(self.ctx, 1 if on else 0))
 
     def last_kernel_ms(self, which: int) -> float:
+        """which: 0 stage 1, 1 the whole solve, 2 the one-wave fused kernel, 3 the overflow
+        workgroup kernel (mpcqp.h)"""
         return float(lib().mpcqp_last_kernel_ms(self.ctx, which))
+
+    def kernel_ms_sum(self, which: int):
+        """(sum of ms, launches) of slot `which` since the previous call (the last 64 at most)"""
+        n = C.c_int(0)
+        ms = float(lib().mpcqp_kernel_ms_sum(self.ctx, which, C.byref(n)))
+        return ms, n.value
 
 
 def decode_key(key: int):

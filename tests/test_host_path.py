@@ -1,0 +1,88 @@
+"""The controller's host-pointer tick (mpcqp_batch_solve_host, what ConvexMpc::solve and
+compat/MPCController.h call once per MPC tick; include/MPCController.h:178-180): pinned staging,
+one copy each way, the step captured into a HIP graph per batch size and overflow-list parity.
+Checked bit-for-bit against the device-pointer path on the same inputs (same kernels), and the
+overflow instances against the oracle (U <= 1e-8 max(1, |U|))."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def host_solve(eng, p, b):
+    from mpcqp._lib import lib
+    B = b["x0"].shape[0]
+    nV = p["nu"] * p["N"]
+    ins = [np.ascontiguousarray(b[k]) for k in ("x0", "xref", "lin", "contact")]
+    out = dict(U=np.full(B * nV, np.nan), cost=np.full(B, np.nan), status=np.full(B, 99, np.int32),
+               iters=np.full(B, -1, np.int32))
+    ptr = lambda a: C.c_void_p(a.ctypes.data)
+    rc = lib().mpcqp_batch_solve_host(eng.ctx, B, *[ptr(a) for a in ins],
+                                      *[ptr(out[k]) for k in ("U", "cost", "status", "iters")])
+    assert rc == 0
+    out["U"] = out["U"].reshape(B, nV)
+    return out
+
+
+def device_solve(eng, b):
+    d = eng.upload(b)
+    eng.solve(d)
+    eng.sync()
+    return {k: d[k].cpu().numpy() for k in ("U", "cost", "status", "iters")}
+
+
+def same(a, b):
+    for k in ("U", "cost", "status", "iters"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+@pytest.mark.parametrize("B", [1, 16, 37])
+def test_host_tick_equals_device_path(gpu, B):
+    """repeated host ticks (graph replays) equal the device path exactly"""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("B")
+    b = mpcqp.make_batch(p, B, seed=101 + B)
+    eng = BatchEngine(p)
+    ref = device_solve(eng, b)
+    for _ in range(3):
+        same(host_solve(eng, p, b), ref)
+    eng.close()
+
+
+def test_host_tick_overflow_parities(gpu, orc):
+    """double-support instances need the workgroup kernel: the host path then captures one
+    graph per overflow-list parity; host ticks interleaved with device-path solves on the same
+    context keep the lists consistent, and the overflow instances match the oracle"""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("B")
+    B = 16
+    b = mpcqp.make_batch(p, B, seed=5, gait="mixed")
+    nf = np.array([3 * bin(int(c)).count("1") for c in b["contact"]])
+    assert (nf > 30).any() and (nf <= 30).any()
+    eng = BatchEngine(p)
+    ref = device_solve(eng, b)
+    for i in range(5):
+        same(host_solve(eng, p, b), ref)
+        if i % 2:
+            same(device_solve(eng, b), ref)
+    o = orc.srbm_batch(p, b["x0"], b["xref"], b["lin"], b["contact"])
+    assert np.all(ref["status"] == 0) and np.all(o["status"] == 0)
+    sc = np.maximum(1.0, np.abs(o["U"]).max(axis=1))
+    assert np.all(np.abs(ref["U"] - o["U"]).max(axis=1) <= 1e-8 * sc)
+    eng.close()
+
+
+def test_host_tick_batch_size_change(gpu):
+    """a new batch size re-captures; going back re-captures again (one cached size)"""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("B")
+    eng = BatchEngine(p)
+    for B in (16, 3, 64, 16):
+        b = mpcqp.make_batch(p, B, seed=B)
+        same(host_solve(eng, p, b), device_solve(eng, b))
+    eng.close()
