@@ -178,6 +178,11 @@ int mpcqp_ctx_reserve(mpcqp_ctx *ctx, int B);
  * max_free <= 30: config B and the literal 13/3/10) */
 int mpcqp_ctx_fast_path(const mpcqp_ctx *ctx);
 
+/* Staged entry points (stage 1 / stage 2 below, mpcqp_batch_solve_qp): the stand-alone solve
+ * holds 64 free variables per instance (more: per-instance status MPCQP_ERR_BAD_DIMS).  On a
+ * MPCQP_MODEL_DENSE context with more than 64 inputs (every input is free there) they return
+ * MPCQP_ERR_BAD_DIMS; mpcqp_batch_solve(_host / _select) serve such contexts (k_dense_wg).
+ * A MPCQP_MODEL_LITERAL context needs u_min < u_max (mpcqp_ctx_create: MPCQP_ERR_BAD_ARG). */
 /* stage 1: linearise + discretise.  AB [B][nx*(nx+nu)] = [Ad | Bd] column-major */
 int mpcqp_batch_discretize(mpcqp_ctx *ctx, int B, const double *lin, double *AB);
 /* stage 2: condense + solve from AB, fused (H stays on chip) */

@@ -140,7 +140,7 @@ __device__ __forceinline__ void half_argmin(double &v, int &idx) {
     int ei, oi;
     row_pair(v, ev, ov);
     row_pair(idx, ei, oi);
-    const bool take = ov < ev || (ov == ev && oi < ei);
+    const bool take = (ov < ev) | ((ov == ev) & (oi < ei));
     v = take ? ov : ev;
     idx = take ? oi : ei;
 }

@@ -127,7 +127,7 @@ __device__ __forceinline__ uint64_t gait_mask_half(int N, double Ts, double phas
 // lane j of this lane's 16-lane row (DPP row_newbcast; j constant after unrolling)
 __device__ __forceinline__ int row_bcast_u32(int v, int j) {
     switch (j) {
-#define MPCQP_RB(i) case i: return __builtin_amdgcn_update_dpp(0, v, 0x150 + i, 0xf, 0xf, false);
+#define MPCQP_RB(i) case i: return __builtin_amdgcn_mov_dpp(v, 0x150 + i, 0xf, 0xf, false);
         MPCQP_RB(0) MPCQP_RB(1) MPCQP_RB(2) MPCQP_RB(3) MPCQP_RB(4) MPCQP_RB(5) MPCQP_RB(6)
         MPCQP_RB(7) MPCQP_RB(8) MPCQP_RB(9) MPCQP_RB(10) MPCQP_RB(11) MPCQP_RB(12) MPCQP_RB(13)
         MPCQP_RB(14) MPCQP_RB(15)
@@ -572,9 +572,16 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     }
     auto blo_of = [&](int sb) { return MODEL == 1 ? a.u_min : ((sb & 4) ? a.fz_min : -a.fxy_max); };
     auto bhi_of = [&](int sb) { return MODEL == 1 ? -a.u_max : ((sb & 4) ? -a.fz_max : -a.fxy_max); };
+    const double blo = blo_of(stb), bhi = bhi_of(stb);  // (bit 2 of stb never changes)
+    const double tlo = -kFeasTol * (1.0 + fabs(blo)), thi = -kFeasTol * (1.0 + fabs(bhi));
     bool done = !ok2;
     bool fresh = true;
     int p = 0;
+    // the partial multiplier of the constraint being added (slot q), in every lane of the half
+    double uadd = 0.0;
+    // a zero double (the masked reads of the R^-1 product point here)
+    constexpr int oZ = Lay::oRow + 4 * NP;
+    if (kRinv && hl == 0) D[oZ] = 0.0;
     MPCQP_SUB_INIT(tsub);
 #ifdef MPCQP_STAMPS
     unsigned long long npass = 0;  // passes of this wavefront (diagnostic slot 2)
@@ -601,7 +608,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 for (int c = 0; c < NF; ++c) {
                     rowbuf[c] = Jr[c];
                 }
-                rowbuf[NP - 1] = lower ? x - blo_of(stb) : -x - bhi_of(stb);
+                rowbuf[NP - 1] = lower ? x - blo : -x - bhi;
             }
             wave_sync();
             dj = (hl < nf) ? sg * rowbuf[hl] : 0.0;
@@ -610,11 +617,13 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 // r = R^-1 d(0:q): lane i < q takes row i of R^-1 (column-major packed, (i, j)
                 // at lrow(j) + i: consecutive lanes, consecutive addresses) against the
                 // published d (uniform address per half); independent products, no chain
+                // (masked terms read the zero slot: an address select instead of value selects)
                 const int qmax = max(__builtin_amdgcn_readlane(q, 0), __builtin_amdgcn_readlane(q, kHalf));
                 double r2[2] = {0.0, 0.0};
                 for (int j = 0; j < qmax; ++j) {
-                    const double rij = Ri[lrow(j) + hl], dv = rowbuf[j];
-                    r2[j & 1] += (hl <= j && j < q) ? rij * dv : 0.0;
+                    const double rij = D[hl <= j ? Lay::oR + lrow(j) + hl : oZ];
+                    const double dv = D[j < q ? Lay::oRow + j : oZ];
+                    r2[j & 1] = fma(rij, dv, r2[j & 1]);
                 }
                 r = (hl < q) ? sg * (r2[0] + r2[1]) : 0.0;
             }
@@ -623,6 +632,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             if (iters >= max_iter) { status = ST_ITER_LIMIT; done = true; }
         }
         MPCQP_SUB(tsub, 0);
+        MPCQP_CUT(a.cut, 20);
         const bool stepping = go && !done;
         if (stepping) {
             ++iters;
@@ -661,21 +671,23 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             if (isinf(t)) { status = ST_INFEASIBLE; done = true; }
         }
         MPCQP_SUB(tsub, 1);
+        MPCQP_CUT(a.cut, 21);
         const bool moving = stepping && !done;
         bool add = false;
         if (moving) {
-            const double uq = hread_k(u, q);
+            const double uq = uadd;
             if (!isinf(t2)) {
                 if (hl < nf) x += t * z;
                 fval += t * zn * (0.5 * t + uq);
             }
             if (hl < q) u -= t * r;
-            if (hl == q) u += t;
+            uadd += t;
+            if (hl == q) u = uadd;
             add = !isinf(t2) && t2 <= t1;
             if (add) {
                 // ---- add p: R column q = (d_0..d_{q-1}, r_qq); the reflection vector v = d2
                 //      - |d2| e_q goes to rowbuf (which holds d2 / sg), v = sg rowbuf
-                const double dq = hread_k(dj, q);
+                const double dq = sg * rowbuf[q];  // d_q: slot q is not zeroed (only j < q)
                 double rqq = dq, vq = 0.0;
                 if (zq > 0.0) {  // otherwise d2 = d_q e_q: no reflection, r_qq = d_q
                     const double nrm = sqrt(zn);
@@ -791,20 +803,20 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         }
         wave_sync();
         MPCQP_SUB(tsub, 2);
+        MPCQP_CUT(a.cut, 22);
         if (!done && fresh) {
             // ---- most violated inactive bound (lowest id on ties): before the first step and
             //      right after every add, so a half's last add also ends its solve (no checking
             //      pass of its own, no update of J that nothing reads)
             double best = INFINITY;
             int bid = 0x7fffffff;
-            const double blo = blo_of(stb), bhi = bhi_of(stb);
             if (stb & 1) {
                 const double s_ = x - blo;
-                if (s_ < -kFeasTol * (1.0 + fabs(blo))) { best = s_; bid = hl; }
+                if (s_ < tlo) { best = s_; bid = hl; }
             }
             if (stb & 2) {
                 const double s_ = -x - bhi;
-                if (s_ < -kFeasTol * (1.0 + fabs(bhi)) && s_ < best) { best = s_; bid = hl + nf; }
+                if ((s_ < thi) & (s_ < best)) { best = s_; bid = hl + nf; }
             }
             half_argmin(best, bid);
             if (bid == 0x7fffffff) {
@@ -812,6 +824,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             } else {
                 p = bid;
                 if (hl == q) u = 0.0;
+                uadd = 0.0;
                 fresh = false;
             }
         }
@@ -853,6 +866,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         }
         wave_sync();
         MPCQP_SUB(tsub, 3);
+        MPCQP_CUT(a.cut, 23);
     }
     MPCQP_SUB_FLUSH(a.stamps, tsub);
 #ifdef MPCQP_STAMPS

@@ -808,6 +808,9 @@ int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
         m->model != MPCQP_MODEL_DENSE)
         return MPCQP_ERR_BAD_ARG;
     if (m->model == MPCQP_MODEL_DENSE && !(m->u_min < m->u_max)) return MPCQP_ERR_BAD_ARG;
+    // literal model: every input is free (u_min < u_max); the fused kernels read a fixed input
+    // as 0, which an empty box (u_min == u_max) would contradict
+    if (m->model == MPCQP_MODEL_LITERAL && !(m->u_min < m->u_max)) return MPCQP_ERR_BAD_ARG;
     if (m->constraints != MPCQP_CONS_BOX && m->constraints != MPCQP_CONS_FRICTION)
         return MPCQP_ERR_BAD_ARG;
     const int nfmax = m->max_free > 0 ? m->max_free : m->nu * m->N;
@@ -1217,10 +1220,19 @@ static SolveArgs batch_solve_args(mpcqp_ctx *c, int B, const double *H, const do
     return a;
 }
 
+// The stand-alone (generic) solve holds 64 free variables.  A dense-model context frees every
+// input (u_min < u_max is required), so above 64 inputs no instance can be served there: the
+// staged entry points refuse it (mpcqp_batch_solve runs k_dense_wg instead).
+static bool generic_solve_unfit(const mpcqp_ctx *c) {
+    const int nfmax = c->m.max_free > 0 ? c->m.max_free : c->m.nu * c->m.N;
+    return c->m.model == MPCQP_MODEL_DENSE && std::min(nfmax, c->m.nu * c->m.N) > kWave;
+}
+
 int mpcqp_batch_solve_qp(mpcqp_ctx *c, int B, const double *H, const double *f,
                          const uint64_t *contact, double *U, double *cost, int *status,
                          int *iters) {
     if (!c || !H || !f || !U || !cost || !status || !iters || B < 0) return MPCQP_ERR_BAD_ARG;
+    if (generic_solve_unfit(c)) return MPCQP_ERR_BAD_DIMS;
     if (c->m.model == MPCQP_MODEL_SRBM && !contact) return MPCQP_ERR_BAD_ARG;
     if (B == 0) return MPCQP_OK;
     hipSetDevice(c->device);
@@ -1278,6 +1290,7 @@ int mpcqp_batch_condense_solve(mpcqp_ctx *c, int B, const double *AB, const doub
     if (!c || !AB || !x0 || !xref || !U || !cost || !status || !iters || B < 0)
         return MPCQP_ERR_BAD_ARG;
     if (c->m.model == MPCQP_MODEL_SRBM && !contact) return MPCQP_ERR_BAD_ARG;
+    if (!(c->fast && c->fk.cs) && generic_solve_unfit(c)) return MPCQP_ERR_BAD_DIMS;
     if (B == 0) return MPCQP_OK;
     hipSetDevice(c->device);
     if (c->fast && c->fk.cs) {

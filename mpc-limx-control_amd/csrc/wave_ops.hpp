@@ -34,9 +34,11 @@ constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
 constexpr int kDppHalfMirror = 0x141; // lane i <- lane 7-i within each 8
 constexpr int kDppMirror = 0x140;     // lane i <- lane 15-i within each 16
 
+// mov_dpp (no tied `old` operand): every control used here reads a valid lane for every lane,
+// or (bound_ctrl) writes 0 where it does not, so no register needs pre-loading with an old value
 template <int CTRL>
 __device__ __forceinline__ int dpp(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
 }
 template <int CTRL>
 __device__ __forceinline__ double dpp(double v) {
@@ -50,24 +52,24 @@ __device__ __forceinline__ double dpp(double v) {
 template <int CTRL>
 __device__ __forceinline__ double dpp_z(double v) {
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xf, 0xf, true);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, true);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffll), CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xf, 0xf, true);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
 // lane l gets lane l + 1's value (DPP wave_shl:1, crosses rows; lane 63 gets 0)
 __device__ __forceinline__ double wave_next(double v) {
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), 0x130, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xf, 0xf, false);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffll), 0x130, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0x130, 0xf, 0xf, true);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
 // lane l gets lane l - 1's value (DPP wave_shr:1, crosses rows; lane 0 gets 0)
 __device__ __forceinline__ double wave_prev(double v) {
     const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), 0x138, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xf, 0xf, false);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffll), 0x138, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0x138, 0xf, 0xf, true);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
@@ -134,7 +136,8 @@ template <int CTRL, bool MIN>
 __device__ __forceinline__ void arg_step(double &v, int &idx) {
     const double ov = dpp<CTRL>(v);
     const int oi = dpp<CTRL>(idx);
-    const bool take = MIN ? (ov < v || (ov == v && oi < idx)) : (ov > v || (ov == v && oi < idx));
+    // bitwise, not short-circuit: no branch per step
+    const bool take = MIN ? ((ov < v) | ((ov == v) & (oi < idx))) : ((ov > v) | ((ov == v) & (oi < idx)));
     v = take ? ov : v;
     idx = take ? oi : idx;
 }

@@ -43,6 +43,7 @@
 #pragma once
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -107,7 +108,24 @@ class BasicMPC {
         calculateGait(iter);
         computeFootPlacement(finalPosition);
         computeSupportFootForce(state, iter);
+        // the reference's swing-leg command (cmd.q from Pinocchio IK, :134-175,195) is not
+        // built: cmd goes back as passed, and this says so at run time
+        if (++untouched_ticks_ == 1 && warnUntouchedCmd)
+            std::fprintf(stderr, "[mpcqp] MPC::run: the swing-leg command path (Pinocchio IK, "
+                                 "include/MPCController.h:134-175) is not implemented; cmd is "
+                                 "returned unmodified (cmdWritten() == false)\n");
     }
+
+    // The reference's run() also writes cmd.q for the swing leg (include/MPCController.h:
+    // 134-175,195: Pinocchio IK on the TRON1 URDF, which the reference repository does not
+    // hold; SURVEY.md 2 #3 puts it out of scope).  run() here leaves cmd as passed: callers that
+    // publish cmd check cmdWritten() (always false) or kWritesSwingCommand;
+    // untouchedCmdTicks() counts the ticks that returned cmd unmodified, and the first one prints
+    // a line to stderr unless warnUntouchedCmd is cleared before it.
+    static constexpr bool kWritesSwingCommand = false;
+    bool cmdWritten() const { return kWritesSwingCommand; }
+    long long untouchedCmdTicks() const { return untouched_ticks_; }
+    bool warnUntouchedCmd = true;
 
     Param param;
     Estimator estimates;
@@ -257,6 +275,7 @@ class BasicMPC {
     uint64_t contact_ = 0;
     double cost_ = 0.0;
     int status_ = -1, choice_ = -1;
+    long long untouched_ticks_ = 0;
 };
 
 }  // namespace mpcqp

@@ -94,5 +94,9 @@ int main(int argc, char **argv) {
         std::printf("\n");
     }
     std::fclose(fp);
+    // the swing-leg command path is not built: run() must say so, and leave cmd as passed
+    if (mpc.cmdWritten() || mpc.untouchedCmdTicks() != T) return 6;
+    for (float v : cmd.tau)
+        if (v != 0.0f) return 7;
     return 0;
 }

@@ -181,6 +181,8 @@ def test_cpp_mpc_controller_tick_matches_oracle(gpu, orc, exes, tmp_path, litera
     r = subprocess.run([exes["mpc_controller"], str(N), str(T), str(literal), str(ncand), str(f)],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
+    # cmd left as passed (swing IK out of scope), said once on stderr
+    assert r.stderr.count("[mpcqp] MPC::run: the swing-leg command path") == 1, r.stderr
     rows = [ln.split() for ln in r.stdout.strip().splitlines()]
     assert len(rows) == T
     left_off, right_off = mpcqp.static_foot_offsets()

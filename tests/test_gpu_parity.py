@@ -602,6 +602,44 @@ def test_overflow_full_size_mixed_gait(gpu, orc):
 
 
 # ------------------------------------------------------------- config E: the dense model
+def test_dense_staged_solve_refused(gpu):
+    """a dense (config E) context frees all 96 inputs, beyond the 64 of the stand-alone
+    solve, so the staged entry points return BAD_DIMS instead of OK with every instance failing;
+    mpcqp_batch_solve still serves it (k_dense_wg)"""
+    import mpcqp
+    from mpcqp._lib import MpcqpError
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("E")
+    batch = mpcqp.make_batch(p, 4, seed=3)
+    eng = BatchEngine(p)
+    d = eng.upload(batch)
+    H, f = eng.condense(d)
+    with pytest.raises(MpcqpError) as e:
+        eng.solve_qp(d, H, f)
+    assert e.value.code == 1
+    AB = eng.discretize(d)
+    with pytest.raises(MpcqpError) as e:
+        eng.condense_solve(d, AB)
+    assert e.value.code == 1
+    eng.solve(d)
+    eng.sync()
+    assert np.all(d["status"].cpu().numpy() == 0)
+    eng.close()
+
+
+def test_literal_empty_input_box_refused(gpu):
+    """the literal model with u_min == u_max (every input fixed) is refused at
+    create: the fused kernels read fixed inputs as 0"""
+    import mpcqp
+    from mpcqp._lib import MpcqpError
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("L", N=10)
+    p["u_min"] = p["u_max"] = 2.0
+    with pytest.raises(MpcqpError) as e:
+        BatchEngine(p)
+    assert e.value.code == 6
+
+
 def test_dense_condense_vs_oracle(gpu, orc):
     """config E (24/6/16 whole-body model, dense Q/R/P): the generic condensing kernel
     (k_condense: Pade expm + Phi chain, full H to HBM) against the oracle's literal dense
