@@ -85,7 +85,8 @@ struct PairLayout {
     static constexpr int oRow = (oR + NR + 1) & ~1;      // buf | colb | rot (2 NP) | 1/R(j,j)
     static constexpr int eLate = oRow + 5 * NP;
     static constexpr int oCt = ((eMid > eLate ? eMid : eLate) + 1) & ~1;  // contact mask (u64)
-    static constexpr int nDoubles = oCt + 2;
+    static constexpr int oDump = oCt + 2;  // sink of the H build's masked-off stores
+    static constexpr int nDoubles = oDump + 1;
     static constexpr size_t bytes =
         (sizeof(double) * nDoubles + sizeof(int) * (NF + NV) + 15) & ~(size_t)15;
     static constexpr size_t lds_bytes = 2 * bytes;  // both halves
@@ -360,11 +361,10 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         const int vi = fid[hl], ki = vi / NU, ci = vi % NU;
         double s = 0.0;
 #pragma unroll
-        for (int m = 1; m <= N; ++m) {  // m > ki; unrolled so the loads issue together
-            if (m > ki) {
-                const double beta = (double)(m - 1 - ki) + 0.5;
-                s += UV[(m * 2 + 0) * NU + ci] + beta * UV[(m * 2 + 1) * NU + ci];
-            }
+        for (int m = 1; m <= N; ++m) {  // m > ki; unrolled, branch-free: the loads issue together
+            const double beta = (double)(m - 1 - ki) + 0.5;
+            const double tm = UV[(m * 2 + 0) * NU + ci] + beta * UV[(m * 2 + 1) * NU + ci];
+            s += (m > ki) ? tm : 0.0;
         }
         gp = 2.0 * s;
     }
@@ -373,57 +373,79 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     if (ok) {
         // one lane per block pair (ki >= kj); the beta sums once per block
         constexpr int NPAIR = N * (N + 1) / 2;
-        int ki = 0, kj = hl;
-        while (kj > ki) { kj -= ki + 1; ++ki; }
+        constexpr int NFT = NU / 3;
+        static_assert(NU % 3 == 0, "inputs are force triples");
         for (int bp = hl; bp < NPAIR; bp += kHalf) {
+            // bp = ki (ki + 1) / 2 + kj, row-major over ki >= kj (closed form, corrected)
+            int ki = (int)((__builtin_sqrtf(8.0f * (float)bp + 1.0f) - 1.0f) * 0.5f);
+            ki += ((ki + 1) * (ki + 2) / 2 <= bp) ? 1 : 0;
+            ki -= (ki * (ki + 1) / 2 > bp) ? 1 : 0;
+            const int kj = bp - ki * (ki + 1) / 2;
             double c, si, sj, sij;
             beta_sums(ki + 1, N - 1, ki, kj, c, si, sj, sij);
             const double bi = (double)(N - 1 - ki) + 0.5, bj = (double)(N - 1 - kj) + 0.5;
             const double bij = bi * bj;
+            const double rf = (ki == kj) ? 1.0 : 0.0;  // R on the diagonal blocks (exact: fma by 1)
             // the free inputs of a step come in whole force triples (a foot in contact has
             // all three components free: the fast path's bounds guarantee it), so the block
-            // is a set of 3x3 foot-pair sub-blocks with consecutive positions
-            constexpr int NFT = NU / 3;
-            static_assert(NU % 3 == 0, "inputs are force triples");
-            int pI[NFT], pJ[NFT];
+            // is a set of 3x3 foot-pair sub-blocks with consecutive positions.  The triples of
+            // each step are compacted (slot a: foot fI[a] at position pI[a], -1 past the step's
+            // count), so a sub-block slot no lane of the wave has is skipped as a whole: one
+            // stance foot per step (config B) runs one 3x3 sub-block per block pair, not four
+            int pI[NFT], pJ[NFT], fI[NFT], fJ[NFT];
 #pragma unroll
-            for (int s = 0; s < NFT; ++s) {
-                pI[s] = pos[ki * NU + 3 * s];
-                pJ[s] = pos[kj * NU + 3 * s];
+            for (int t = 0; t < NFT; ++t) { pI[t] = pJ[t] = -1; fI[t] = fJ[t] = 0; }
+            int nI = 0, nJ = 0;
+#pragma unroll
+            for (int s_ = 0; s_ < NFT; ++s_) {
+                const int p_i = pos[ki * NU + 3 * s_], p_j = pos[kj * NU + 3 * s_];
+#pragma unroll
+                for (int t = 0; t < NFT; ++t) {
+                    const bool ti = p_i >= 0 && nI == t, tj = p_j >= 0 && nJ == t;
+                    pI[t] = ti ? p_i : pI[t];
+                    fI[t] = ti ? s_ : fI[t];
+                    pJ[t] = tj ? p_j : pJ[t];
+                    fJ[t] = tj ? s_ : fJ[t];
+                }
+                nI += p_i >= 0 ? 1 : 0;
+                nJ += p_j >= 0 ? 1 : 0;
             }
 #pragma unroll
-            for (int si = 0; si < NFT; ++si) {
+            for (int ta = 0; ta < NFT; ++ta) {
 #pragma unroll
-                for (int sj = 0; sj < NFT; ++sj) {
-                    if (pI[si] < 0 || pJ[sj] < 0) continue;
+                for (int tb = 0; tb < NFT; ++tb) {
+                    if (pI[ta] < 0 || pJ[tb] < 0) continue;
 #pragma unroll
                     for (int a3 = 0; a3 < 3; ++a3) {
 #pragma unroll
                         for (int b3 = 0; b3 < 3; ++b3) {
-                            const int pp = pI[si] + a3, qq = pJ[sj] + b3;
-                            const int ci = 3 * si + a3, cj = 3 * sj + b3;
-                            if (pp >= qq) {
-                                const double *So = S + (cj * NU + ci) * 4;
-                                double v = c * So[0] + sij * So[1];
-                                v += So[2] + bij * So[3];
-                                if (ki == kj) v += Rm[cj * NU + ci];
-                                Hb[lrow(pp) + qq] = 2.0 * v;
-                            }
+                            const int pp = pI[ta] + a3, qq = pJ[tb] + b3;
+                            const int ci = 3 * fI[ta] + a3, cj = 3 * fJ[tb] + b3;
+                            // branch-free: the strictly upper entries of a diagonal block go
+                            // to the dump slot
+                            const double *So = S + (cj * NU + ci) * 4;
+                            double v = c * So[0] + sij * So[1];
+                            v += So[2] + bij * So[3];
+                            v = fma(rf, Rm[cj * NU + ci], v);
+                            Hb[pp >= qq ? lrow(pp) + qq : Lay::oDump - Lay::oR] = 2.0 * v;
                         }
                     }
                 }
             }
-            kj += kHalf;
-            while (kj > ki) { kj -= ki + 1; ++ki; }
         }
+    }
+    // rows without a free variable (past nf, or a half with nothing to solve) are identity
+    // rows of the padded H_FF: written into the packed buffer (rare: only such waves pay), so
+    // every lane then loads its row unmasked (entries right of the diagonal are never read)
+    const bool pad = !ok || hl >= nf;
+    if (__ballot(pad && hl < NF) != 0ull) {
+        if (pad && hl < NF)
+            for (int q = 0; q <= hl; ++q) Hb[lrow(hl) + q] = (q == hl) ? 1.0 : 0.0;
     }
     wave_sync();
     double h[NF];
 #pragma unroll
-    for (int q = 0; q < NF; ++q) {
-        const bool in = ok && hl < nf && q < nf && q <= hl;
-        h[q] = in ? Hb[lrow(hl) + q] : ((q == hl) ? 1.0 : 0.0);
-    }
+    for (int q = 0; q < NF; ++q) h[q] = Hb[lrow(hl) + q];
     wave_sync();
     MPCQP_STAMP(a.stamps, 3, tst);
     MPCQP_CUT(a.cut, 3);
