@@ -67,10 +67,53 @@ __device__ __forceinline__ double srbm_entry(int i, int j, const double *lin, do
     return 0.0;
 }
 
+// sin and cos of x: Cody-Waite reduction by pi/2 in three parts (pio2_1 has 33 significant
+// bits, so n pio2_1 and x - n pio2_1 are exact for |n| < 2^20) and fdlibm's __kernel_sin /
+// __kernel_cos minimax polynomials on |r| <= pi/4 (< 1 ulp, as libm).  ~40 VALU instead of the
+// library's ~150 (which also carries the Payne-Hanek path); |x| >= 2^19 goes to the library.
+__device__ __forceinline__ void fast_sincos(double x, double *sp, double *cp) {
+    if (!(fabs(x) < 524288.0)) {
+        sincos(x, sp, cp);
+        return;
+    }
+    const double fn = rint(x * 6.36619772367581382433e-01);
+    const int n = (int)fn;
+    double r = fma(-fn, 1.57079632673412561417e+00, x);
+    r = fma(-fn, 6.07710050630396597660e-11, r);
+    r = fma(-fn, 2.02226624879595063154e-21, r);
+    const double z = r * r;
+    // __kernel_sin(r, 0, 0)
+    const double ps = 8.33333333332248946124e-03 +
+                      z * (-1.98412698298579493134e-04 +
+                           z * (2.75573137070700676789e-06 +
+                                z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)));
+    const double sn = r + (z * r) * (-1.66666666666666324348e-01 + z * ps);
+    // __kernel_cos(r, 0)
+    const double pc =
+        z * (4.16666666666666019037e-02 +
+             z * (-1.38888888888741095749e-03 +
+                  z * (2.48015872894767294178e-05 +
+                       z * (-2.75573143513906633035e-07 +
+                            z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+    const double ar = fabs(r);
+    double cs;
+    if (ar < 0.3) {
+        cs = 1.0 - (0.5 * z - z * pc);
+    } else {
+        const double qx = ar > 0.78125 ? 0.28125
+                                       : __hiloint2double(__double2hiint(ar) - 0x00200000, 0);
+        cs = (1.0 - qx) - ((0.5 * z - qx) - z * pc);
+    }
+    const int q = n & 3;
+    const double s0 = (q & 1) ? cs : sn, c0 = (q & 1) ? sn : cs;
+    *sp = (q & 2) ? -s0 : s0;
+    *cp = ((q + 1) & 2) ? -c0 : c0;
+}
+
 // Rz(yaw) and the world-frame inverse inertia Iw^-1 = Rz Ib^-1 Rz' (column-major)
 __device__ __forceinline__ void srbm_rot_inertia(double yaw, const double *Ibinv, double &cy,
                                                  double &sy, double *Iwi) {
-    sincos(yaw, &sy, &cy);
+    fast_sincos(yaw, &sy, &cy);
     const double Rz[9] = {cy, sy, 0.0, -sy, cy, 0.0, 0.0, 0.0, 1.0};
     double Tm[9];
 #pragma unroll
@@ -116,7 +159,7 @@ __device__ __forceinline__ void wave_build_model(const ModelConst &mc, const dou
     double Iwi[9];
     double cy = 1.0, sy = 0.0;
     if (mc.model == 0) {
-        sincos(lin[0], &sy, &cy);
+        fast_sincos(lin[0], &sy, &cy);
         // Iw^-1 = Rz Ib^-1 Rz'
         const double Rz[9] = {cy, sy, 0.0, -sy, cy, 0.0, 0.0, 0.0, 1.0};
         double Tm[9];

@@ -276,45 +276,105 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     MPCQP_STAMP(a.stamps, 0, tst);
     MPCQP_CUT(a.cut, 1);
     if (work) {
-        // ---- model: lane i < NX holds row i of Ac; X0 = Bc Ts and X1 = (Ac Ts) X0 on their
-        //      support rows, A x0, A^2 x0 (A = Ac Ts).  Same products, in the same order, as the
-        //      one-QP kernel (the zero terms it adds are exact).
-        double Iwi[9];
-        double cy = 1.0, sy = 0.0;
-        if (MODEL == 0) srbm_rot_inertia(lin[0], a.Ibinv, cy, sy, Iwi);
-        auto entry = [&](int i, int j) -> double {  // [Ac | Bc](i, j)
-            return MODEL == 0 ? srbm_entry(i, j, lin, cy, sy, Iwi, a.mass)
-                              : literal_entry(i, j, lin, a.mass);
-        };
-        const double Ts = a.Ts;
-        double arow[NX];
+        if constexpr (MODEL == 0) {
+            // ---- SRBM model, rows written out: Ac's nonzeros are Theta' = Rz' omega (rows 0-2),
+            //      p' = v (3-5), v_z' = g (11); Bc's are omega' = Iw^-1 [r_f]x f (6-8) and
+            //      v' = f / m (9-11).  Each product keeps the one-QP kernel's operation order
+            //      (its zero terms are exact), without evaluating the 13 x 19 entries per lane.
+            double Iwi[9];
+            double cy = 1.0, sy = 0.0;
+            srbm_rot_inertia(lin[0], a.Ibinv, cy, sy, Iwi);
+            const double Ts = a.Ts, im = 1.0 / a.mass;
+            if (hl >= Sup::x0lo && hl < Sup::x0hi) {  // X0 = Bc Ts, rows 6-11
+                const int ii = hl - 6;
+                const double e0 = ii == 0 ? 1.0 : 0.0, e1 = ii == 1 ? 1.0 : 0.0,
+                             e2 = ii == 2 ? 1.0 : 0.0;
+                const double w0 = e0 * Iwi[0] + e1 * Iwi[1] + e2 * Iwi[2];
+                const double w1 = e0 * Iwi[3] + e1 * Iwi[4] + e2 * Iwi[5];
+                const double w2 = e0 * Iwi[6] + e1 * Iwi[7] + e2 * Iwi[8];
 #pragma unroll
-        for (int k = 0; k < NX; ++k) arow[k] = entry(hl, k);
-        if (hl >= Sup::x0lo && hl < Sup::x0hi) {
-#pragma unroll
-            for (int c = 0; c < NU; ++c) X0[c * SD + hl - Sup::x0lo] = entry(hl, NX + c) * Ts;
-        }
-        if (hl < NX) {
-            double s = 0.0;
-#pragma unroll
-            for (int k = 0; k < NX; ++k) s += arow[k] * x0g[k];
-            Ax[hl] = s * Ts;
-        }
-        wave_sync();
-        if (hl >= Sup::x1lo && hl < Sup::x1hi) {
-#pragma unroll
-            for (int c = 0; c < NU; ++c) {
-                double s = 0.0;
-#pragma unroll
-                for (int k = Sup::x0lo; k < Sup::x0hi; ++k) s += arow[k] * X0[c * SD + k - Sup::x0lo];
-                X1[c * SD + hl - Sup::x1lo] = s * Ts;
+                for (int c = 0; c < NU; ++c) {
+                    const int ft = c / 3, comp = c % 3;
+                    const double r0 = lin[1 + 3 * ft], r1 = lin[2 + 3 * ft], r2 = lin[3 + 3 * ft];
+                    double xa, xb, xc;  // column comp of [r]x
+                    if (comp == 0) { xa = 0.0; xb = r2; xc = -r1; }
+                    else if (comp == 1) { xa = -r2; xb = 0.0; xc = r0; }
+                    else { xa = r1; xb = -r0; xc = 0.0; }
+                    const double om = w0 * xa + w1 * xb + w2 * xc;
+                    const double vv = (ii - 3 == comp) ? im : 0.0;
+                    X0[c * SD + ii] = (ii < 3 ? om : vv) * Ts;
+                }
             }
-        }
-        if (hl < NX) {
-            double s = 0.0;
+            // row hl of Ac times a vector y (y6, y7, y8 broadcast, yh = y[hl + 6], y12)
+            auto arow_dot = [&](double y6, double y7, double y8, double yh, double y12) {
+                const double s0 = fma(sy, y7, cy * y6), s1 = fma(cy, y7, -sy * y6);
+                double v = 0.0;
+                v = hl == 0 ? s0 : v;
+                v = hl == 1 ? s1 : v;
+                v = hl == 2 ? y8 : v;
+                v = (hl >= 3 && hl < 6) ? yh : v;
+                v = hl == 11 ? y12 : v;
+                return v;
+            };
+            const int h6 = hl + 6 < NX ? hl + 6 : NX - 1;
+            if (hl < NX)
+                Ax[hl] = arow_dot(x0g[6], x0g[7], x0g[8], x0g[h6], x0g[12]) * Ts;
+            wave_sync();
+            if (hl >= Sup::x1lo && hl < Sup::x1hi) {  // X1 = (Ac Ts) X0, rows 0-5
 #pragma unroll
-            for (int k = 0; k < NX; ++k) s += arow[k] * Ax[k];
-            A2x[hl] = s * Ts;
+                for (int c = 0; c < NU; ++c) {
+                    const double *Xc = X0 + c * SD;
+                    const double s0 = fma(sy, Xc[1], cy * Xc[0]), s1 = fma(cy, Xc[1], -sy * Xc[0]);
+                    double v = Xc[hl < 6 ? hl : 0];
+                    v = hl == 0 ? s0 : v;
+                    v = hl == 1 ? s1 : v;
+                    v = hl == 2 ? Xc[2] : v;
+                    X1[c * SD + hl - Sup::x1lo] = v * Ts;
+                }
+            }
+            if (hl < NX)
+                A2x[hl] = arow_dot(Ax[6], Ax[7], Ax[8], Ax[h6], Ax[12]) * Ts;
+        } else {
+            // ---- model: lane i < NX holds row i of Ac; X0 = Bc Ts and X1 = (Ac Ts) X0 on their
+            //      support rows, A x0, A^2 x0 (A = Ac Ts).  Same products, in the same order, as the
+            //      one-QP kernel (the zero terms it adds are exact).
+            double Iwi[9];
+            double cy = 1.0, sy = 0.0;
+            if (MODEL == 0) srbm_rot_inertia(lin[0], a.Ibinv, cy, sy, Iwi);
+            auto entry = [&](int i, int j) -> double {  // [Ac | Bc](i, j)
+                return MODEL == 0 ? srbm_entry(i, j, lin, cy, sy, Iwi, a.mass)
+                                  : literal_entry(i, j, lin, a.mass);
+            };
+            const double Ts = a.Ts;
+            double arow[NX];
+    #pragma unroll
+            for (int k = 0; k < NX; ++k) arow[k] = entry(hl, k);
+            if (hl >= Sup::x0lo && hl < Sup::x0hi) {
+    #pragma unroll
+                for (int c = 0; c < NU; ++c) X0[c * SD + hl - Sup::x0lo] = entry(hl, NX + c) * Ts;
+            }
+            if (hl < NX) {
+                double s = 0.0;
+    #pragma unroll
+                for (int k = 0; k < NX; ++k) s += arow[k] * x0g[k];
+                Ax[hl] = s * Ts;
+            }
+            wave_sync();
+            if (hl >= Sup::x1lo && hl < Sup::x1hi) {
+    #pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    double s = 0.0;
+    #pragma unroll
+                    for (int k = Sup::x0lo; k < Sup::x0hi; ++k) s += arow[k] * X0[c * SD + k - Sup::x0lo];
+                    X1[c * SD + hl - Sup::x1lo] = s * Ts;
+                }
+            }
+            if (hl < NX) {
+                double s = 0.0;
+    #pragma unroll
+                for (int k = 0; k < NX; ++k) s += arow[k] * Ax[k];
+                A2x[hl] = s * Ts;
+            }
         }
         MPCQP_CUT(a.cut, 13);
 
