@@ -87,13 +87,19 @@ def _profile_json(name):
         return None
 
 
+def lib_build_id():
+    from mpcqp._lib import lib
+    return lib().mpcqp_build_id().decode()
+
+
 def pmc_traffic(config: str, batch: int):
     """HBM bytes per fused-kernel launch from the committed rocprofv3 PMC summary
-    (tools/profile_run.sh + tools/summarize_profile.py), if it matches this workload."""
+    (tools/profile_run.sh + tools/summarize_profile.py), if it matches this workload; with the
+    summary's tag and the source hash of the library it was measured on."""
     t = _profile_json("pmc_traffic.json")
     if not t or t.get("config") != config or t.get("batch") != batch:
-        return None, None
-    return t.get("hbm_bytes_per_launch"), t.get("tag")
+        return None, None, None
+    return t.get("hbm_bytes_per_launch"), t.get("tag"), t.get("lib_build_id")
 
 
 def pmc_executed(config: str, batch: int):
@@ -579,7 +585,8 @@ def main():
         # whole solve in the timed steps (mpc_ms) also hold the overflow launch
         k_ms = kern[eng.fused_kernel]["ms"] if eng.fused_kernel in kern else mpc_ms
         achieved = f_qp * B / (k_ms * 1e-3) / 1e12
-        traffic, traffic_tag = pmc_traffic(args.config, B)
+        traffic, traffic_tag, traffic_lib = pmc_traffic(args.config, B)
+        build = lib_build_id()
         kms = {k: v["ms"] for k, v in kern.items()}
         kms["mpcqp_batch_solve" + ("_select" if fused else "") +
             " (timed steps, events around the call)"] = mpc_ms
@@ -594,6 +601,8 @@ def main():
                     unit="TFLOP/s", frac=achieved / FP64_PEAK_TFLOPS, traffic=traffic,
                     traffic_source=(f"profiles/{traffic_tag}_summary.json (rocprofv3 PMC, "
                                     "2 x FETCH_SIZE + WRITE_SIZE)") if traffic else None,
+                    traffic_lib_build_id=traffic_lib, lib_build_id=build,
+                    traffic_matches_library=(traffic_lib == build) if traffic else None,
                     algorithmic_bytes_per_launch=algorithmic_bytes(p["nx"], p["nu"], p["N"]) * B,
                     algorithmic_flops_per_qp=f_qp,
                     basis="SURVEY.md 8d algorithmic flops (F_fixed + F_iter x mean iters) per "
@@ -611,6 +620,7 @@ def main():
                                       "instruction count: EXEC-masked lanes included, an " \
                                       "upper bound; + MFMA ops)"
             roof["executed_tag"] = ex.get("tag")
+            roof["executed_matches_library"] = ex.get("lib_build_id") == build
         out["roofline"] = roof
         if weak:
             cfg["weak"] = weak

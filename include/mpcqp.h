@@ -308,6 +308,9 @@ double mpcqp_kernel_ms_sum(mpcqp_ctx *ctx, int which, int *count);
 int mpcqp_debug_phase_cycles(mpcqp_ctx *ctx, uint64_t *out, int n);
 
 const char *mpcqp_status_string(int status);
+/* hash of the sources this library was built from (profiles/ record it beside each counter
+ * pass, so a summary can be matched to the library that was benchmarked) */
+const char *mpcqp_build_id(void);
 int mpcqp_device_count(void);
 
 #ifdef __cplusplus

@@ -6,11 +6,17 @@
 #include "dense_wg.hpp"
 #include "fast_kernels.hpp"
 
+// waves per SIMD the register budget is sized for (2: what the 72.8 KB of LDS per workgroup
+// allows, 256 registers; 1: 512 registers incl. AGPRs, one workgroup per CU)
+#ifndef MPCQP_DENSE_W
+#define MPCQP_DENSE_W 2
+#endif
+
 namespace mpcqp {
 namespace {
 
 template <int NX, int NU, int N>
-__global__ void __launch_bounds__(WgShape<NU * N>::THREADS, 2) k_dense_wg(MpcArgs a) {
+__global__ void __launch_bounds__(WgShape<NU * N>::THREADS, MPCQP_DENSE_W) k_dense_wg(MpcArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_d[];
     // one workgroup per QP (grid = B): no grid-stride loop, so nothing is hoisted out of a loop
     // and kept live across the whole body

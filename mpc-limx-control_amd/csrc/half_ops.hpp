@@ -130,6 +130,45 @@ __device__ __forceinline__ double half_max(double v) {
     row_pair(v, e, o);
     return fmax(e, o);
 }
+// minimum within each half (compare / select: no canonicalising v_min_f64 under IEEE mode)
+__device__ __forceinline__ double half_min(double v) {
+    double o = dpp<kDppXor1>(v);
+    v = o < v ? o : v;
+    o = dpp<kDppXor2>(v);
+    v = o < v ? o : v;
+    o = dpp<kDppHalfMirror>(v);
+    v = o < v ? o : v;
+    o = dpp<kDppMirror>(v);
+    v = o < v ? o : v;
+    double e, od;
+    row_pair(v, e, od);
+    return od < e ? od : e;
+}
+// two sums in one pass (the DPP chains interleave)
+__device__ __forceinline__ void half_sum2(double &a, double &b) {
+    a += dpp<kDppXor1>(a);
+    b += dpp<kDppXor1>(b);
+    a += dpp<kDppXor2>(a);
+    b += dpp<kDppXor2>(b);
+    a += dpp<kDppHalfMirror>(a);
+    b += dpp<kDppHalfMirror>(b);
+    a += dpp<kDppMirror>(a);
+    b += dpp<kDppMirror>(b);
+    double e, o;
+    row_pair(a, e, o);
+    a = e + o;
+    row_pair(b, e, o);
+    b = e + o;
+}
+// (value, lane) minimum within each half, lowest lane on ties: the minimum by compare/select,
+// then one ballot of the lanes holding it (no index carried through the DPP steps).  A half
+// whose values are all +inf gets lane 0x7fffffff.
+__device__ __forceinline__ int half_argmin_lane(double &v) {
+    const double m = half_min(v);
+    const uint32_t hit = half_ballot(v == m);
+    v = m;
+    return m == INFINITY ? 0x7fffffff : (int)__builtin_ctz(hit);
+}
 // lexicographic (value, index) minimum within each half
 __device__ __forceinline__ void half_argmin(double &v, int &idx) {
     arg_step<kDppXor1, true>(v, idx);

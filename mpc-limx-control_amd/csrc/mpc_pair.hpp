@@ -531,10 +531,14 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         //      separate Cholesky then inverse sweep.
         if (hl < NF) colb[hl] = gv;
         wave_sync();
+        // (branch-free: every lane reads colb -- a uniform address, two values per b128 -- and
+        //  selects, instead of a predicated read per element)
+        const bool gl = hl == kHalf - 1;
 #pragma unroll
         for (int l = 0; l < NF; ++l) {
-            Jr[l] = (hl == l) ? 1.0 : 0.0;
-            Jr[l] = (hl == kHalf - 1) ? colb[l] : Jr[l];
+            double cbl = colb[l];
+            pin(cbl);  // (keeps the load unconditional: LLVM would sink it into a branch)
+            Jr[l] = gl ? cbl : ((hl == l) ? 1.0 : 0.0);
         }
         double piv = hbcast<0>(h[0]);
         bool bad = !(piv > 0.0);
@@ -548,14 +552,18 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
 #pragma unroll
         for (int k = 0; k < NF; k += CB) {
             double lk[CB], ikc[CB];
+            double bc[CB][CB];  // bc[c][c2] = L(k + c, k + c2), broadcast once: the panel update
+                                // and the inverse sweep's column both use it
             ikc[0] = ik;
             lk[0] = h[k] * ik;
             h[k] = lk[0];
 #pragma unroll
             for (int c = 1; c < CB; ++c) {
 #pragma unroll
-                for (int c2 = 0; c2 < c; ++c2)
-                    h[k + c] -= lk[c2] * hbcast(lk[c2], k + c);  // panel column c2's update
+                for (int c2 = 0; c2 < c; ++c2) {
+                    bc[c][c2] = hbcast(lk[c2], k + c);
+                    h[k + c] -= lk[c2] * bc[c][c2];  // panel column c2's update
+                }
                 const double pc = hbcast(h[k + c], k + c);
                 bad |= !(pc > 0.0);
                 ikc[c] = rsqrt_nr(pc);
@@ -577,7 +585,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
 #pragma unroll
             for (int c = 0; c < CB; ++c) {
 #pragma unroll
-                for (int c2 = 0; c2 < c; ++c2) Jr[k + c] -= hbcast(lk[c2], k + c) * Jr[k + c2];
+                for (int c2 = 0; c2 < c; ++c2) Jr[k + c] -= bc[c][c2] * Jr[k + c2];
                 Jr[k + c] *= ikc[c];
             }
             wave_sync();
@@ -673,7 +681,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         ++npass;
 #endif
         double dj = 0.0, sp = 0.0, z = 0.0, zn = 0.0, zq = 0.0, r = 0.0, t1 = INFINITY,
-               t2 = INFINITY, t = 0.0, sg = 1.0, beta = 0.0;
+               t2 = INFINITY, t = 0.0, sg = 1.0, beta = 0.0, dqv = 0.0;
         int kslot = 0x7fffffff, a_ = 0;
         bool lower = true;
         // a pass either steps on the selected constraint p or (first pass) only selects
@@ -718,10 +726,14 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         const bool stepping = go && !done;
         if (stepping) {
             ++iters;
-            double dd = hl < nf ? dj * dj : 0.0;
-            zn = (hl >= q && hl < nf) ? dj * dj : 0.0;
+            // |d(0:q)|^2 and |d(q+1:nf)|^2 in one two-sum pass; zn = |d2|^2 = zq + d_q^2 and
+            // dd = |d|^2 = zn + the first part
+            double sq = hl < q ? dj * dj : 0.0;
             zq = (hl > q && hl < nf) ? dj * dj : 0.0;
-            half_sum3(dd, zn, zq);
+            half_sum2(sq, zq);
+            dqv = q < nf ? sg * rowbuf[q] : 0.0;  // d_q: slot q is not zeroed (only j < q)
+            zn = fma(dqv, dqv, zq);
+            const double dd = zn + sq;
             double z4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int j = 0; j < NF; ++j) {
@@ -744,8 +756,8 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                     }
                 }
                 const double rmax = half_max(hl < q ? fabs(r) : 0.0);
-                if (hl < q && r > kRTol * rmax) { t1 = u / r; kslot = hl; }
-                half_argmin(t1, kslot);
+                if (hl < q && r > kRTol * rmax) t1 = u / r;
+                kslot = half_argmin_lane(t1);
             }
             const bool dep = !(zn > kDepTol * dd);
             t2 = dep ? INFINITY : -sp / zn;
@@ -769,7 +781,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             if (add) {
                 // ---- add p: R column q = (d_0..d_{q-1}, r_qq); the reflection vector v = d2
                 //      - |d2| e_q goes to rowbuf (which holds d2 / sg), v = sg rowbuf
-                const double dq = sg * rowbuf[q];  // d_q: slot q is not zeroed (only j < q)
+                const double dq = dqv;
                 double rqq = dq, vq = 0.0;
                 if (zq > 0.0) {  // otherwise d2 = d_q e_q: no reflection, r_qq = d_q
                     const double nrm = sqrt(zn);
@@ -891,16 +903,21 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             //      right after every add, so a half's last add also ends its solve (no checking
             //      pass of its own, no update of J that nothing reads)
             double best = INFINITY;
-            int bid = 0x7fffffff;
+            bool upb = false;  // the lane's candidate is its upper bound (id hl + nf)
             if (stb & 1) {
                 const double s_ = x - blo;
-                if (s_ < tlo) { best = s_; bid = hl; }
+                if (s_ < tlo) best = s_;
             }
             if (stb & 2) {
                 const double s_ = -x - bhi;
-                if ((s_ < thi) & (s_ < best)) { best = s_; bid = hl + nf; }
+                if ((s_ < thi) & (s_ < best)) { best = s_; upb = true; }
             }
-            half_argmin(best, bid);
+            // lowest id among the lanes at the minimum: a lower bound (id hl) before any upper
+            // bound (hl + nf), each by lowest lane
+            const double bm = half_min(best);
+            const uint32_t hit = half_ballot(best == bm), hitl = half_ballot(best == bm && !upb);
+            const int bid = bm == INFINITY ? 0x7fffffff
+                          : hitl ? (int)__builtin_ctz(hitl) : (int)__builtin_ctz(hit) + nf;
             if (bid == 0x7fffffff) {
                 done = true;  // optimal
             } else {

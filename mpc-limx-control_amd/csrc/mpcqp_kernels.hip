@@ -563,6 +563,11 @@ struct mpcqp_ctx {
 
 extern "C" {
 
+#ifndef MPCQP_BUILD_ID
+#define MPCQP_BUILD_ID "unversioned"
+#endif
+const char *mpcqp_build_id(void) { return MPCQP_BUILD_ID; }
+
 const char *mpcqp_status_string(int s) {
     switch (s) {
         case MPCQP_OK: return "OK";

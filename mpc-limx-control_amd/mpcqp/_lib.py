@@ -32,7 +32,7 @@ EXPORTS = [
     "mpcqp_batch_solve_gait", "mpcqp_batch_select_state", "mpcqp_batch_plant_srbm",
     "mpcqp_rollout", "mpcqp_fk_feet", "mpcqp_kf_update", "mpcqp_ctx_reserve",
     "mpcqp_ctx_fk_feet_host", "mpcqp_set_warm_start",
-    "mpcqp_status_string", "mpcqp_device_count",
+    "mpcqp_status_string", "mpcqp_device_count", "mpcqp_build_id",
 ]
 
 
@@ -104,6 +104,8 @@ def lib():
     L.mpcqp_kernel_ms_sum.restype = C.c_double
     L.mpcqp_status_string.argtypes = [i]
     L.mpcqp_status_string.restype = C.c_char_p
+    L.mpcqp_build_id.argtypes = []
+    L.mpcqp_build_id.restype = C.c_char_p
     L.mpcqp_device_count.argtypes = []
     _lib = L
     return L

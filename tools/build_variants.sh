@@ -1,19 +1,20 @@
 #!/bin/bash
 # Build A/B variants of the paired kernel's translation unit (CPU; hipcc cross-compiles):
-#   tools/build_variants.sh name1:"-DFLAG=1" name2:"" ...
+#   [TU=fast_dense] tools/build_variants.sh name1:"-DFLAG=1" name2:"" ...
 # Each variant relinks the release objects with its own fast_pair.o into
 # lib/libmpcqp_<name>.so (time them on the GPU box with tools/ab_libs.sh) and prints the
 # compiler's VGPR spill count for the config B kernel.
 R=$(cd "$(dirname "$0")/.." && pwd)
+TU=${TU:-fast_pair}
 cd "$R/mpc-limx-control_amd" || exit 1
 HF="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -w -mllvm -pragma-unroll-threshold=1000000 -mllvm -amdgpu-sched-strategy=max-ilp"
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
-  ( mkdir -p "build/$name" && /opt/rocm/bin/hipcc $HF $flags -c -o "build/$name/fast_pair.o" csrc/fast_pair.hip && \
-    /opt/rocm/bin/hipcc $HF -shared -o "lib/libmpcqp_$name.so" $(ls build/rel/*.o | grep -v fast_pair.o) \
-        "build/$name/fast_pair.o" && \
+  ( mkdir -p "build/$name" && /opt/rocm/bin/hipcc $HF $flags -c -o "build/$name/$TU.o" csrc/$TU.hip && \
+    /opt/rocm/bin/hipcc $HF -shared -o "lib/libmpcqp_$name.so" $(ls build/rel/*.o | grep -v $TU.o) \
+        "build/$name/$TU.o" && \
     echo "$name $(/opt/rocm/bin/hipcc $HF $flags -Rpass-analysis=kernel-resource-usage --cuda-device-only -c \
-        -o "/tmp/ru_$name.o" csrc/fast_pair.hip 2>&1 | grep -A10 'pairILi6ELi10ELi0ELb0' | grep -E 'VGPRs Spill' \
+        -o "/tmp/ru_$name.o" csrc/$TU.hip 2>&1 | grep -E 'VGPRs Spill' | head -1 \
         | sed 's/.*remark://;s/\[-R.*//')" ) &
 done
 wait

@@ -19,11 +19,22 @@ import statistics as st
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def per_dispatch(path, kernel):
-    """{counter: median over dispatches of `kernel` of the per-dispatch total}"""
+def kernel_tag(name):
+    i = name.find("k_")
+    j = name.find(">", i)
+    return name[i:j + 1] if i >= 0 and j > i else name
+
+
+def per_dispatch(path, kernel, grid=None):
+    """{counter: median over dispatches of `kernel` (exact instantiation when it names one,
+    e.g. 'k_mpc_pair<6, 10, 0, false>', else a substring) at `grid` threads of the
+    per-dispatch total}"""
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(path)):
-        if kernel not in r["Kernel_Name"]:
+        name = r["Kernel_Name"]
+        if ("<" in kernel and kernel_tag(name) != kernel) or kernel not in name:
+            continue
+        if grid is not None and int(r["Grid_Size"]) != grid:
             continue
         acc[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
     return {c: st.median(v.values()) for c, v in acc.items()}, \
@@ -38,10 +49,12 @@ def main():
     ap.add_argument("--config", default="B")
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--out", default="pmc_flops.json")
+    ap.add_argument("--grid", type=int, default=None, help="threads per launch (default: all)")
     a = ap.parse_args()
-    sq, n = per_dispatch(os.path.join(a.prof, "sq", "run_counter_collection.csv"), a.kernel)
+    sq, n = per_dispatch(os.path.join(a.prof, "sq", "run_counter_collection.csv"), a.kernel, a.grid)
     try:
-        gr, _ = per_dispatch(os.path.join(a.prof, "grbm", "run_counter_collection.csv"), a.kernel)
+        gr, _ = per_dispatch(os.path.join(a.prof, "grbm", "run_counter_collection.csv"), a.kernel,
+                             a.grid)
     except OSError:
         gr = {}
     g = lambda k: sq.get(k, 0.0)
@@ -49,7 +62,9 @@ def main():
     upper = 64.0 * (2 * g("SQ_INSTS_VALU_FMA_F64") + g("SQ_INSTS_VALU_MUL_F64") +
                     g("SQ_INSTS_VALU_ADD_F64") + g("SQ_INSTS_VALU_TRANS_F64")) + \
         512.0 * g("SQ_INSTS_VALU_MFMA_MOPS_F64")
-    out = dict(tag=a.tag, kernel=a.kernel, config=a.config, batch=a.batch, file=a.out,
+    import summarize_profile
+    out = dict(tag=a.tag, lib_build_id=summarize_profile.lib_build_id(), kernel=a.kernel,
+               grid=a.grid, config=a.config, batch=a.batch, file=a.out,
                counters=sq, dispatches=n, grbm=gr,
                executed_flops_per_launch=executed, lane_flops_upper_bound=upper,
                mfma_flops_per_launch=512.0 * g("SQ_INSTS_VALU_MFMA_MOPS_F64"))

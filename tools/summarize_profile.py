@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Summarize a tools/profile_run.sh output directory into profiles/:
-  <tag>_kernel_stats.csv   rocprofv3 --stats summary (copied verbatim)
-  <tag>_summary.json       per-kernel average duration + PMC HBM traffic per launch
+  <tag>_kernel_stats.csv   rocprofv3 --stats summary (copied verbatim; it averages by kernel NAME
+                           over every grid and workload of the run)
+  <tag>_summary.json       per (kernel instantiation, grid, workgroup) average duration from the
+                           kernel trace, the headline group (--kernel at --grid), PMC HBM traffic
+                           per launch, and the source hash of the profiled library
   pmc_traffic.json         the k_mpc traffic figure bench.py reports as roofline.traffic
 HBM bytes follow MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE are KiB,
 collected in separate passes; on gfx950 FETCH_SIZE counts half of the bytes of a coalesced
@@ -32,6 +35,31 @@ def counter(path, kernel, grid):
     return st.median(v) if v else None, len(v)
 
 
+def lib_build_id():
+    """source hash compiled into the library that was profiled (mpcqp_build_id)"""
+    try:
+        import ctypes
+        L = ctypes.CDLL(os.path.join(ROOT, "mpc-limx-control_amd", "lib", "libmpcqp.so"))
+        L.mpcqp_build_id.restype = ctypes.c_char_p
+        return L.mpcqp_build_id().decode()
+    except (OSError, AttributeError):
+        return None
+
+
+def dispatch_groups(trace):
+    """per (kernel instantiation, grid, workgroup) average duration over its dispatches in the
+    kernel trace -- the rocprofv3 --stats summary averages by NAME, mixing grids and workloads"""
+    g = {}
+    for r in csv.DictReader(open(trace)):
+        key = (kernel_tag(r["Kernel_Name"]), int(r["Grid_Size_X"]), int(r["Workgroup_Size_X"]))
+        g.setdefault(key, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3)
+    out = []
+    for (k, grid, wg), v in sorted(g.items(), key=lambda kv: -sum(kv[1])):
+        out.append(dict(kernel=k, grid_threads=grid, workgroup=wg, calls=len(v),
+                        avg_us=st.mean(v), median_us=st.median(v), min_us=min(v), max_us=max(v)))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("prof")
@@ -48,17 +76,22 @@ def main():
     kern = {r["Name"]: dict(calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]),
                             pct=float(r["Percentage"])) for r in csv.DictReader(open(stats))}
     grid = a.grid or 32 * a.batch
+    groups = dispatch_groups(os.path.join(a.prof, "trace", "run_kernel_trace.csv"))
+    head = [g for g in groups if g["kernel"] == a.kernel and g["grid_threads"] == grid]
     fetch, nf = counter(os.path.join(a.prof, "fetch", "run_counter_collection.csv"), a.kernel, grid)
     write, nw = counter(os.path.join(a.prof, "write", "run_counter_collection.csv"), a.kernel, grid)
     traffic = None
     if fetch is not None and write is not None:
         traffic = 2.0 * fetch * 1024 + write * 1024
-    summ = dict(tag=a.tag, kernel=a.kernel, grid=grid, config=a.config, batch=a.batch, kernels=kern,
+    summ = dict(tag=a.tag, lib_build_id=lib_build_id(), kernel=a.kernel, grid=grid, config=a.config,
+                batch=a.batch, headline=head[0] if head else None, dispatch_groups=groups,
+                kernels_by_name_mixed_grids=kern,
                 fetch_size_kib_median=fetch, write_size_kib_median=write, fetch_samples=nf,
                 write_samples=nw, hbm_bytes_per_launch=traffic,
                 correction="reads = 2 x FETCH_SIZE (gfx950 half-count), writes = WRITE_SIZE")
     json.dump(summ, open(os.path.join(out, f"{a.tag}_summary.json"), "w"), indent=1)
     json.dump(dict(config=a.config, batch=a.batch, kernel=a.kernel, grid=grid, tag=a.tag,
+                   lib_build_id=summ["lib_build_id"],
                    hbm_bytes_per_launch=traffic, read_bytes=2.0 * fetch * 1024 if fetch else None,
                    write_bytes=write * 1024 if write else None), open(os.path.join(out, "pmc_traffic.json"), "w"),
               indent=1)
