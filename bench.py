@@ -316,6 +316,7 @@ def time_config(config, B, seed, steps=10, warmup=2, gait=None, device=0):
         out["mfma_tflops"] = ex["mfma_flops_per_launch"] / (ms * 1e-3) / 1e12
         out["mfma_busy_frac"] = ex.get("mfma_busy_frac")
         out["pmc_source"] = f"profiles/pmc_flops_{config}.json ({ex.get('tag')})"
+        out["pmc_matches_library"] = ex.get("lib_build_id") == lib_build_id()
     tr = _profile_json(f"pmc_traffic_{config}.json")
     if tr and tr.get("batch") == B and gait is None and tr.get("hbm_bytes_per_launch"):
         # HBM bytes of this kernel (2 x FETCH_SIZE + WRITE_SIZE, separate PMC passes) against
@@ -325,6 +326,7 @@ def time_config(config, B, seed, steps=10, warmup=2, gait=None, device=0):
         out["algorithmic_bytes_per_launch"] = alg
         out["traffic_over_algorithmic"] = tr["hbm_bytes_per_launch"] / alg
         out["traffic_source"] = f"profiles/pmc_traffic_{config}.json ({tr.get('tag')})"
+        out["traffic_matches_library"] = tr.get("lib_build_id") == lib_build_id()
     eng.close()
     return out
 

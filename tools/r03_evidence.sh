@@ -1,0 +1,35 @@
+#!/bin/bash
+# Round-3 evidence set at the current library (GPU box, repo root), all tagged TAG:
+#   gpurun_out/ev_TAG/bench.json           the default bench line (cpu baseline, per-config)
+#   gpurun_out/ev_TAG/B/{trace,fetch,write} headline k_mpc_pair: kernel trace + HBM passes
+#   gpurun_out/ev_TAG/B_flops/{sq,grbm}    executed FP64 / MFMA counters of the headline
+#   gpurun_out/ev_TAG/{C,E}/...            the same for configs C (65,536) and E (16,384)
+#   gpurun_out/ev_TAG/Bst/trace            k_mpc_pair + k_mpc_wg at B standing (overflow path)
+# Summaries are written on the CPU afterwards (tools/summarize_*.py).  Counter passes never
+# share a run with trace domains.
+set -o pipefail
+TAG=${1:-r03}
+O=gpurun_out/ev_$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+R=$(pwd)
+run() {  # name timeout cmd...
+  local n=$1 t=$2; shift 2
+  timeout -k 10 $t "$@" > $O/$n.log 2>&1 || { echo "$n failed"; tail -n 5 $O/$n.log; exit 1; }
+}
+run bench 500 python3 bench.py
+grep '^{' $O/bench.log > $O/bench.json
+HB="--steps 20 --warmup 3 --no-cpu-baseline --no-per-config"
+run B_trace 300 rocprofv3 --kernel-trace --stats -d $R/$O/B/trace -o run --output-format csv -- python3 bench.py $HB
+run B_fetch 200 rocprofv3 --pmc FETCH_SIZE -d $R/$O/B/fetch -o run --output-format csv -- python3 bench.py $HB
+run B_write 200 rocprofv3 --pmc WRITE_SIZE -d $R/$O/B/write -o run --output-format csv -- python3 bench.py $HB
+run B_flops 400 bash tools/pmc_flops.sh $O/B_flops $HB
+for spec in "C:--config C" "E:--config E --global-batch 16384"; do
+  c=${spec%%:*}; a="${spec#*:} --steps 5 --warmup 1 --no-cpu-baseline --no-per-config --weak-batch 0"
+  run ${c}_trace 300 rocprofv3 --kernel-trace --stats -d $R/$O/$c/trace -o run --output-format csv -- python3 bench.py $a
+  run ${c}_fetch 200 rocprofv3 --pmc FETCH_SIZE -d $R/$O/$c/FETCH_SIZE -o run --output-format csv -- python3 bench.py $a
+  run ${c}_write 200 rocprofv3 --pmc WRITE_SIZE -d $R/$O/$c/WRITE_SIZE -o run --output-format csv -- python3 bench.py $a
+  run ${c}_flops 400 bash tools/pmc_flops.sh $O/${c}_flops $a
+done
+run Bst_trace 300 rocprofv3 --kernel-trace --stats -d $R/$O/Bst/trace -o run --output-format csv -- python3 tools/time_kernel.py --configs B --gait standing --reps 10
+echo "evidence $TAG OK"

@@ -78,8 +78,11 @@ def main():
     grid = a.grid or 32 * a.batch
     groups = dispatch_groups(os.path.join(a.prof, "trace", "run_kernel_trace.csv"))
     head = [g for g in groups if g["kernel"] == a.kernel and g["grid_threads"] == grid]
-    fetch, nf = counter(os.path.join(a.prof, "fetch", "run_counter_collection.csv"), a.kernel, grid)
-    write, nw = counter(os.path.join(a.prof, "write", "run_counter_collection.csv"), a.kernel, grid)
+    fetch = write = None
+    nf = nw = 0
+    if os.path.exists(os.path.join(a.prof, "fetch")):  # trace-only runs have no counter passes
+        fetch, nf = counter(os.path.join(a.prof, "fetch", "run_counter_collection.csv"), a.kernel, grid)
+        write, nw = counter(os.path.join(a.prof, "write", "run_counter_collection.csv"), a.kernel, grid)
     traffic = None
     if fetch is not None and write is not None:
         traffic = 2.0 * fetch * 1024 + write * 1024
@@ -90,11 +93,12 @@ def main():
                 write_samples=nw, hbm_bytes_per_launch=traffic,
                 correction="reads = 2 x FETCH_SIZE (gfx950 half-count), writes = WRITE_SIZE")
     json.dump(summ, open(os.path.join(out, f"{a.tag}_summary.json"), "w"), indent=1)
-    json.dump(dict(config=a.config, batch=a.batch, kernel=a.kernel, grid=grid, tag=a.tag,
+    if traffic is not None:
+        json.dump(dict(config=a.config, batch=a.batch, kernel=a.kernel, grid=grid, tag=a.tag,
                    lib_build_id=summ["lib_build_id"],
                    hbm_bytes_per_launch=traffic, read_bytes=2.0 * fetch * 1024 if fetch else None,
                    write_bytes=write * 1024 if write else None), open(os.path.join(out, "pmc_traffic.json"), "w"),
-              indent=1)
+                  indent=1)
     print(json.dumps(summ, indent=1)[:1500])
 
 

@@ -10,7 +10,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from summarize_profile import counter  # noqa: E402
+from summarize_profile import counter, lib_build_id  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -29,6 +29,7 @@ def main():
     if fetch is None or write is None:
         sys.exit(f"no launches of {a.kernel} at grid {a.grid} in {a.dir}")
     out = dict(config=a.config, batch=a.batch, kernel=a.kernel, grid=a.grid, tag=a.tag,
+               lib_build_id=lib_build_id(),
                read_bytes=2.0 * fetch * 1024, write_bytes=write * 1024,
                hbm_bytes_per_launch=2.0 * fetch * 1024 + write * 1024,
                fetch_samples=nf, write_samples=nw,
