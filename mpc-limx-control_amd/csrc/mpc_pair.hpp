@@ -80,7 +80,8 @@ struct PairLayout {
     static constexpr int eUV = oUV + (N + 1) * 2 * NU;
     static constexpr int oS = oU + ((HB > eUV - oU ? HB : eUV - oU) + 1) / 2 * 2;  // [NU*NU][4]
     static constexpr int oRm = oS + 4 * NU * NU;         // R (NU x NU)
-    static constexpr int eMid = oRm + NU * NU;
+    static constexpr int oWq = oRm + NU * NU;            // diag Q, diag P (NX each)
+    static constexpr int eMid = oWq + 2 * NX;
     static constexpr int oR = oU;
     static constexpr int oRow = (oR + NR + 1) & ~1;      // buf | colb | rot (2 NP) | 1/R(j,j)
     static constexpr int eLate = oRow + 5 * NP;
@@ -186,7 +187,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     int *pos = fid + NF;
     double *X0 = D + Lay::oX0, *X1 = D + Lay::oX1, *Ax = D + Lay::oAx, *A2x = D + Lay::oA2x;
     double *xr = D + Lay::oXr, *x0g = D + Lay::oX0v, *UV = D + Lay::oUV;
-    double *S = D + Lay::oS, *Rm = D + Lay::oRm;
+    double *S = D + Lay::oS, *Rm = D + Lay::oRm, *Wq = D + Lay::oWq;
 
     // ---- per-instance inputs: all global loads back to back, then parked in LDS
     double lin[8];
@@ -203,6 +204,8 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         const double ph0 = a.phase[b];
         const double rm0 = (hl < NRM) ? a.rmat[hl] : 0.0;
         const double rm1 = (hl + kHalf < NRM) ? a.rmat[hl + kHalf] : 0.0;
+        const double wq = (hl < 2 * NX) ? (hl < NX ? a.qd[hl] : a.pd[hl - NX]) : 0.0;
+        if (hl < 2 * NX) Wq[hl] = wq;
         if (hl < NX) x0g[hl] = stv;
         if (hl < NRM) Rm[hl] = rm0;
         if (hl + kHalf < NRM) Rm[hl + kHalf] = rm1;
@@ -231,11 +234,13 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         const double x0l = (hl < NX) ? stream_load(a.x0 + (size_t)b * NX + hl) : 0.0;
         const double rm0 = (hl < NRM) ? a.rmat[hl] : 0.0;
         const double rm1 = (hl + kHalf < NRM) ? a.rmat[hl + kHalf] : 0.0;
+        const double wq = (hl < 2 * NX) ? (hl < NX ? a.qd[hl] : a.pd[hl - NX]) : 0.0;
         if (MODEL == 0) contact = stream_load(a.contact + b);
 #pragma unroll
         for (int r = 0; r < RX; ++r)
             if (hl + r * kHalf < NXR) xr[hl + r * kHalf] = v[r];
         if (hl < NX) x0g[hl] = x0l;
+        if (hl < 2 * NX) Wq[hl] = wq;
         if (hl < NRM) Rm[hl] = rm0;
         if (hl + kHalf < NRM) Rm[hl + kHalf] = rm1;
     }
@@ -384,7 +389,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             const int r_ = blk & 1, w_ = blk >> 1;
             const int lo = r_ ? Sup::x1lo : Sup::x0lo;
             const double *Xr = r_ ? X1 : X0;
-            const double *w = w_ ? a.pd : a.qd;
+            const double *w = Wq + (w_ ? NX : 0);  // diag P / Q staged in LDS
             for (int e = hl; e < NRM; e += kHalf) {
                 const int ci = e % NU, cj = e / NU;
                 double acc = 0.0;
@@ -393,19 +398,27 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 S[e * 4 + blk] = acc;
             }
         }
-        // ---- u_m(c) = X0[:,c]' W_m e_m, v_m(c) = X1[:,c]' W_m e_m, m = 1..N
+        // ---- W_m e_m once per (m, support row) -- shared by the NU components -- over the dead
+        //      xref slot (e_m = x0 + m A x0 + m^2 A^2 x0 / 2 - xref_m), then
+        //      u_m(c) = X0[:,c]' W_m e_m, v_m(c) = X1[:,c]' W_m e_m, m = 1..N
+        wave_sync();  // (S read X0 / X1 only; xref is still whole)
+        constexpr int NSUP = 2 * SD;  // support rows of X1 then X0
+        for (int e = hl; e < N * NSUP; e += kHalf) {
+            const int m = 1 + e / NSUP, t = e % NSUP;
+            const int l = t < SD ? Sup::x1lo + t : Sup::x0lo + t - SD;
+            const double md = (double)m, hm2 = 0.5 * md * md;
+            const double wl = Wq[(m < N ? 0 : NX) + l];
+            xr[m * NX + l] = wl * (x0g[l] + md * Ax[l] + hm2 * A2x[l] - xr[m * NX + l]);
+        }
+        wave_sync();
         for (int e = hl; e < N * NU; e += kHalf) {
             const int c = e % NU, m = 1 + e / NU;
-            const double md = (double)m, hm2 = 0.5 * md * md;
-            auto el = [&](int l) {
-                const double wl = (m < N) ? a.qd[l] : a.pd[l];
-                return wl * (x0g[l] + md * Ax[l] + hm2 * A2x[l] - xr[m * NX + l]);
-            };
+            const double *el = xr + m * NX;
             double su = 0.0, sv = 0.0;
 #pragma unroll
-            for (int l = Sup::x0lo; l < Sup::x0hi; ++l) su += X0[c * SD + l - Sup::x0lo] * el(l);
+            for (int l = Sup::x0lo; l < Sup::x0hi; ++l) su += X0[c * SD + l - Sup::x0lo] * el[l];
 #pragma unroll
-            for (int l = Sup::x1lo; l < Sup::x1hi; ++l) sv += X1[c * SD + l - Sup::x1lo] * el(l);
+            for (int l = Sup::x1lo; l < Sup::x1hi; ++l) sv += X1[c * SD + l - Sup::x1lo] * el[l];
             UV[(m * 2 + 0) * NU + c] = su;
             UV[(m * 2 + 1) * NU + c] = sv;
         }
