@@ -102,6 +102,13 @@ __device__ __forceinline__ void wg_pick(const double *red, int o, double &v, int
 // g: g_r on both halves of row r (0 beyond nf).  W: WgLayout<NF>::doubles of LDS.
 // C.L must provide xs (128), cb, st, fid, pos, xfull.  Fills C.{status, x, fval, q, iters};
 // every thread returns x_r of its row.
+// The dual loop keeps R^-1 (column-major packed, (i, j) at lrow(j) + i) instead of R: r = R^-1 d
+// is a product over the slots instead of a back substitution whose every step waits on the
+// previous one (see mpc_pair.hpp for the add / drop updates); 0 keeps R (A/B builds)
+#ifndef MPCQP_WG_RINV
+#define MPCQP_WG_RINV 1
+#endif
+
 template <int NF>
 __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double g, double *W) {
     using Lay = WgLayout<NF>;
@@ -313,7 +320,24 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
         }
         MPCQP_SUB(tsub, 1);
         double r0 = 0.0, r1 = 0.0;  // wave 0: r of slots ln and ln + 64
-        if (wv == 0 && q > 0) {
+        if (MPCQP_WG_RINV && wv == 0 && q > 0) {
+            // r = R^-1 d(0:q): slot i takes row i of R^-1 against the published d (uniform
+            // addresses); independent products in two accumulators per slot
+            double a0[2] = {0.0, 0.0}, a1[2] = {0.0, 0.0};
+#pragma unroll 4
+            for (int j = 0; j < q; ++j) {
+                const double dj = dB[j];
+                const double v0 = (ln <= j) ? Lc[lrow(j) + ln] : 0.0;
+                a0[j & 1] = fma(v0, dj, a0[j & 1]);
+                if constexpr (TWO) {
+                    const double v1 = (ln + 64 <= j) ? Lc[lrow(j) + ln + 64] : 0.0;
+                    a1[j & 1] = fma(v1, dj, a1[j & 1]);
+                }
+            }
+            r0 = (ln < q) ? a0[0] + a0[1] : 0.0;
+            r1 = (TWO && ln + 64 < q) ? a1[0] + a1[1] : 0.0;
+        }
+        if (!MPCQP_WG_RINV && wv == 0 && q > 0) {
             // r = R^-1 d(0:q), back substitution (R packed in LDS, 1/R(j,j) beside it).  The
             // chain from one step to the next is v_readlane -> mul -> FMA in registers: 1/R(j,j)
             // is read out of registers too, and R's columns are prefetched two steps ahead, so
@@ -375,6 +399,8 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
 #pragma unroll
                 for (int t = 0; t < 4; ++t) cc[t] = nc[t];
             }
+        }
+        if (wv == 0 && q > 0) {
             const double rmax = wave_max(fmax(ln < q ? fabs(r0) : 0.0, ln + 64 < q ? fabs(r1) : 0.0));
             double t1 = INFINITY;
             int ks = 0x7fffffff;
@@ -429,13 +455,26 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
                 beta = 2.0 / (vq * vq + zq);
             }
             if (wv == 0) {
-                if (ln < q) Lc[roff(q) + ln] = dB[ln];
-                if (TWO && ln + 64 < q) Lc[roff(q) + ln + 64] = dB[ln + 64];
-                if (ln == 0) {
-                    Lc[roff(q) + q] = rqq;
-                    rinv[q] = 1.0 / rqq;
-                    acts[q] = p;
-                    L.st[p] = 2;
+                if (MPCQP_WG_RINV) {
+                    // R^-1 of [[R, d1], [0, rqq]]: new column q = (-R^-1 d1 / rqq, 1 / rqq), and
+                    // R^-1 d1 is this pass's r (wave 0's r0 / r1)
+                    const double irq = 1.0 / rqq;
+                    if (ln < q) Lc[lrow(q) + ln] = -r0 * irq;
+                    if (TWO && ln + 64 < q) Lc[lrow(q) + ln + 64] = -r1 * irq;
+                    if (ln == 0) {
+                        Lc[lrow(q) + q] = irq;
+                        acts[q] = p;
+                        L.st[p] = 2;
+                    }
+                } else {
+                    if (ln < q) Lc[roff(q) + ln] = dB[ln];
+                    if (TWO && ln + 64 < q) Lc[roff(q) + ln + 64] = dB[ln + 64];
+                    if (ln == 0) {
+                        Lc[roff(q) + q] = rqq;
+                        rinv[q] = 1.0 / rqq;
+                        acts[q] = p;
+                        L.st[p] = 2;
+                    }
                 }
             }
             // the reflector's slot q: written by every wave for its own J update below (LDS is
@@ -460,16 +499,57 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
                 if (ln >= k && ln < q) { us[ln] = un0; acts[ln] = an0; }
                 if (TWO && ln + 64 >= k && ln + 64 < q) { us[ln + 64] = un1; acts[ln + 64] = an1; }
                 if (ln == 0) L.st[dropped] = 1;
-                for (int j = k; j < q - 1; ++j) {
+                if (MPCQP_WG_RINV) {
+                    // R^-1 G' with the rotations that zero row k of R^-1 left of column q-1 (the
+                    // same G as restores R without column k: mpc_pair.hpp), row k deleted and the
+                    // last column dropped; each rotated column j is final once rotated
+                    const int qn = q - 1;
+                    for (int j = ln; j < NF; j += kWave) { rot[2 * j] = 1.0; rot[2 * j + 1] = 0.0; }
+                    wave_sync();
+                    double ra = Lc[lrow(k) + k];
+                    for (int j = k; j < qn; ++j) {
+                        const double rb = Lc[lrow(j + 1) + k];
+                        double c = 1.0, s_ = 0.0;
+                        if (ra != 0.0) {
+                            const double hh = sqrt(ra * ra + rb * rb), ih = 1.0 / hh;
+                            c = rb * ih;
+                            s_ = -ra * ih;
+                            ra = hh;
+                        } else {
+                            ra = rb;
+                        }
+                        const int i0 = ln, i1 = ln + 64;
+                        const double y00 = (i0 <= j) ? Lc[lrow(j) + i0] : 0.0;
+                        const double y10 = (i0 <= j + 1) ? Lc[lrow(j + 1) + i0] : 0.0;
+                        double y01 = 0.0, y11 = 0.0;
+                        if (TWO) {
+                            y01 = (i1 <= j) ? Lc[lrow(j) + i1] : 0.0;
+                            y11 = (i1 <= j + 1) ? Lc[lrow(j + 1) + i1] : 0.0;
+                        }
+                        if (i0 <= j + 1 && i0 != k) Lc[lrow(j) + i0 - (i0 > k ? 1 : 0)] = c * y00 + s_ * y10;
+                        if (i0 <= j + 1) Lc[lrow(j + 1) + i0] = -s_ * y00 + c * y10;
+                        if (TWO) {
+                            if (i1 <= j + 1 && i1 != k) Lc[lrow(j) + i1 - (i1 > k ? 1 : 0)] = c * y01 + s_ * y11;
+                            if (i1 <= j + 1) Lc[lrow(j + 1) + i1] = -s_ * y01 + c * y11;
+                        }
+                        if (ln == 0) {
+                            rot[2 * j] = c;
+                            rot[2 * j + 1] = s_;
+                        }
+                        wave_sync();
+                    }
+                }
+                for (int j = k; !MPCQP_WG_RINV && j < q - 1; ++j) {
                     const double v0 = (ln <= j + 1) ? Lc[roff(j + 1) + ln] : 0.0;
                     const double v1 = (TWO && ln + 64 <= j + 1) ? Lc[roff(j + 1) + ln + 64] : 0.0;
                     if (ln <= j + 1) Lc[roff(j) + ln] = v0;
                     if (TWO && ln + 64 <= j + 1) Lc[roff(j) + ln + 64] = v1;
                 }
                 const int qn = q - 1;
-                for (int j = ln; j < NF; j += kWave) { rot[2 * j] = 1.0; rot[2 * j + 1] = 0.0; }
+                if (!MPCQP_WG_RINV)
+                    for (int j = ln; j < NF; j += kWave) { rot[2 * j] = 1.0; rot[2 * j + 1] = 0.0; }
                 wave_sync();
-                for (int j = k; j < qn; ++j) {
+                for (int j = k; !MPCQP_WG_RINV && j < qn; ++j) {
                     const double a_ = Lc[roff(j) + j], bb = Lc[roff(j) + j + 1];
                     if (bb != 0.0) {
                         const double hh = sqrt(a_ * a_ + bb * bb);
