@@ -56,7 +56,8 @@ struct WgLayout {
     static constexpr int oUs = oRinv + RW;           // slot multipliers u
     static constexpr int oRed = oUs + RW;            // reduction slots
     static constexpr int oAct = oRed + 32;           // slot constraint ids (int)
-    static constexpr int doubles = oAct + RW / 2;
+    static constexpr int oRp = oAct + RW / 2;        // [waves][RW] partial products R^-1 d
+    static constexpr int doubles = oRp + 2 * RW * (RW / 64);
     static_assert(2 * CBW >= 2 * NF, "rotations fit the column buffers");
     // the blocked factorisation (chol_mfma.hpp) overlays the whole workspace before the loop
     static constexpr int work = doubles > TileFact<NF>::doubles ? doubles : TileFact<NF>::doubles;
@@ -107,6 +108,16 @@ __device__ __forceinline__ void wg_pick(const double *red, int o, double &v, int
 // previous one (see mpc_pair.hpp for the add / drop updates); 0 keeps R (A/B builds)
 #ifndef MPCQP_WG_RINV
 #define MPCQP_WG_RINV 1
+#endif
+// 1: every wave takes every (2 NWH)-th column of the R^-1 product, the partials meet in LDS
+// behind the barrier that follows anyway and every wave finishes r, max |r| and t1 itself
+#ifndef MPCQP_WG_RSPLIT
+#define MPCQP_WG_RSPLIT 1
+#endif
+// 1: the J products skip 8-column blocks the step leaves untouched -- columns c < q of d2 and
+// of the reflector are zero, and a drop rotates only columns k .. q
+#ifndef MPCQP_WG_SKIP
+#define MPCQP_WG_SKIP 1
 #endif
 
 template <int NF>
@@ -305,10 +316,14 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
         {   // z = J2 d2 (per-half partial sums)
             double z4[4] = {0.0, 0.0, 0.0, 0.0};
             const double *dq = dqB + h * NH;
+            const int qb = __builtin_amdgcn_readfirstlane(q - h * NH);  // first column of d2 here
 #pragma unroll
-            for (int j = 0; j < NH; ++j) {
-                z4[j & 3] += Jr[j] * dq[j];
-                if ((j & 7) == 7) step_fence();
+            for (int b = 0; b < NH; b += 8) {
+                if (!MPCQP_WG_SKIP || b + 7 >= qb) {
+#pragma unroll
+                    for (int j = b; j < b + 8 && j < NH; ++j) z4[j & 3] += Jr[j] * dq[j];
+                }
+                step_fence();
             }
             part[h * RW + r] = (z4[0] + z4[1]) + (z4[2] + z4[3]);
         }
@@ -319,8 +334,36 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             if (ln == 0) { red[8 + 3 * wv] = dd; red[9 + 3 * wv] = zn; red[10 + 3 * wv] = zq; }
         }
         MPCQP_SUB(tsub, 1);
-        double r0 = 0.0, r1 = 0.0;  // wave 0: r of slots ln and ln + 64
-        if (MPCQP_WG_RINV && wv == 0 && q > 0) {
+        double r0 = 0.0, r1 = 0.0;  // wave 0 (every wave with RSPLIT): r of slots ln and ln + 64
+        // the slot multipliers t1 divides, read before the barrier (wave 0 updates them after it)
+        double us0 = 0.0, us1 = 0.0;
+        if (MPCQP_WG_RINV && MPCQP_WG_RSPLIT && q > 0) {
+            // this wave's columns j = wv, wv + 2 NWH, ...; partials to LDS, summed after the
+            // barrier in wave order
+            constexpr int NW = 2 * NWH;
+            double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+            int j = wv;
+            for (; j + NW < q; j += 2 * NW) {
+                const double dj = dB[j], dk = dB[j + NW];
+                a0 = fma((ln <= j) ? Lc[lrow(j) + ln] : 0.0, dj, a0);
+                b0 = fma((ln <= j + NW) ? Lc[lrow(j + NW) + ln] : 0.0, dk, b0);
+                if constexpr (TWO) {
+                    a1 = fma((ln + 64 <= j) ? Lc[lrow(j) + ln + 64] : 0.0, dj, a1);
+                    b1 = fma((ln + 64 <= j + NW) ? Lc[lrow(j + NW) + ln + 64] : 0.0, dk, b1);
+                }
+            }
+            if (j < q) {
+                const double dj = dB[j];
+                a0 = fma((ln <= j) ? Lc[lrow(j) + ln] : 0.0, dj, a0);
+                if constexpr (TWO) a1 = fma((ln + 64 <= j) ? Lc[lrow(j) + ln + 64] : 0.0, dj, a1);
+            }
+            us0 = us[ln];
+            if constexpr (TWO) us1 = us[ln + 64];
+            double *rp = W + Lay::oRp + wv * RW;
+            rp[ln] = a0 + b0;
+            if constexpr (TWO) rp[ln + 64] = a1 + b1;
+        }
+        if (MPCQP_WG_RINV && !MPCQP_WG_RSPLIT && wv == 0 && q > 0) {
             // r = R^-1 d(0:q): slot i takes row i of R^-1 against the published d (uniform
             // addresses); independent products in two accumulators per slot
             double a0[2] = {0.0, 0.0}, a1[2] = {0.0, 0.0};
@@ -400,7 +443,7 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
                 for (int t = 0; t < 4; ++t) cc[t] = nc[t];
             }
         }
-        if (wv == 0 && q > 0) {
+        if (!(MPCQP_WG_RINV && MPCQP_WG_RSPLIT) && wv == 0 && q > 0) {
             const double rmax = wave_max(fmax(ln < q ? fabs(r0) : 0.0, ln + 64 < q ? fabs(r1) : 0.0));
             double t1 = INFINITY;
             int ks = 0x7fffffff;
@@ -413,14 +456,35 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             if (ln == 0) { red[16] = t1; red[17] = (double)ks; }
         }
         __syncthreads();
+        double t1 = INFINITY;
+        int kslot = 0x7fffffff;
+        if (MPCQP_WG_RINV && MPCQP_WG_RSPLIT && q > 0) {
+            const double *rp = W + Lay::oRp;
+            constexpr int NW = 2 * NWH;
+            double v0 = rp[ln], v1 = TWO ? rp[ln + 64] : 0.0;
+#pragma unroll
+            for (int w = 1; w < NW; ++w) {
+                v0 += rp[w * RW + ln];
+                if constexpr (TWO) v1 += rp[w * RW + ln + 64];
+            }
+            r0 = (ln < q) ? v0 : 0.0;
+            r1 = (TWO && ln + 64 < q) ? v1 : 0.0;
+            const double rmax = wave_max(fmax(fabs(r0), fabs(r1)));
+            if (ln < q && r0 > kRTol * rmax) { t1 = us0 / r0; kslot = ln; }
+            if (TWO && ln + 64 < q && r1 > kRTol * rmax) {
+                const double tt = us1 / r1;
+                if (tt < t1) { t1 = tt; kslot = ln + 64; }
+            }
+            wave_argmin(t1, kslot);
+        } else if (q > 0) {
+            t1 = red[16];
+            kslot = (int)red[17];
+        }
         MPCQP_SUB(tsub, 2);
         const double z = part[r] + part[RW + r];
         const double dd = NWH == 2 ? red[8] + red[11] : red[8];
         const double zn = NWH == 2 ? red[9] + red[12] : red[9];
         const double zq = NWH == 2 ? red[10] + red[13] : red[10];
-        double t1 = INFINITY;
-        int kslot = 0x7fffffff;
-        if (q > 0) { t1 = red[16]; kslot = (int)red[17]; }
         const bool dep = !(zn > kDepTol * dd);
         const double t2 = dep ? INFINITY : -sp / zn;
         const double t = t1 < t2 ? t1 : t2;
@@ -585,10 +649,15 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
         if (__builtin_amdgcn_readfirstlane((int)(add && beta != 0.0))) {
             double w4[4] = {0.0, 0.0, 0.0, 0.0};
             const double *v = dqB + h * NH;
+            // the reflector is zero left of the slot just added (q - 1)
+            const int qb = __builtin_amdgcn_readfirstlane(q - 1 - h * NH);
 #pragma unroll
-            for (int j = 0; j < NH; ++j) {
-                w4[j & 3] += Jr[j] * v[j];
-                if ((j & 7) == 7) step_fence();
+            for (int b = 0; b < NH; b += 8) {
+                if (!MPCQP_WG_SKIP || b + 7 >= qb) {
+#pragma unroll
+                    for (int j = b; j < b + 8 && j < NH; ++j) w4[j & 3] += Jr[j] * v[j];
+                }
+                step_fence();
             }
             // partial sums into d2B / tB (dead on the add path), not part: a lagging wave may
             // still be reading this pass's z out of part
@@ -596,41 +665,52 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             __syncthreads();
             const double f = beta * (d2B[r] + tB[r]);
 #pragma unroll
-            for (int j = 0; j < NH; ++j) {
-                Jr[j] -= f * v[j];
-                if ((j & 7) == 7) step_fence();
+            for (int b = 0; b < NH; b += 8) {
+                if (!MPCQP_WG_SKIP || b + 7 >= qb) {
+#pragma unroll
+                    for (int j = b; j < b + 8 && j < NH; ++j) Jr[j] -= f * v[j];
+                }
+                step_fence();
             }
         }
         if (__builtin_amdgcn_readfirstlane((int)!add)) {
-            // J columns: rotations (j, j+1), j = 0 .. NF-2, identity where (c, s) = (1, 0);
-            // half 0 applies 0 .. NH-1 (the last one needs column NH from half 1), then half 1
-            // continues from the carried column NH
-            if (h == 1) d2B[r] = Jr[0];
-            __syncthreads();
-            if (h == 0) {
+            // J columns: rotations (j, j+1), j = 0 .. NF-2, identity where (c, s) = (1, 0) -- all
+            // but j = kslot .. q-1 (q after the drop).  Half 0 applies 0 .. NH-1 (the last one
+            // needs column NH from half 1), then half 1 continues from the carried column NH;
+            // when rotation NH-1 is the identity the halves run at once, no carry.  8-rotation
+            // blocks outside kslot .. q-1 are skipped (uniform branches; the block's loads issue
+            // together)
+            const int jlo = __builtin_amdgcn_readfirstlane(kslot), jhi = __builtin_amdgcn_readfirstlane(q - 1);
+            auto live_blk = [&](int j0, int j1) { return !MPCQP_WG_SKIP || (j1 >= jlo && j0 <= jhi); };
+            auto rot_half = [&](int base) {  // rotations base + j, j = 0 .. NH-2, in registers
 #pragma unroll
-                for (int j = 0; j < NH - 1; ++j) {
-                    const double c = rot[2 * j], s_ = rot[2 * j + 1];
-                    const double y0 = Jr[j], y1 = Jr[j + 1];
-                    Jr[j] = c * y0 + s_ * y1;
-                    Jr[j + 1] = -s_ * y0 + c * y1;
-                }
-                const double c = rot[2 * (NH - 1)], s_ = rot[2 * (NH - 1) + 1];
-                const double y0 = Jr[NH - 1], y1 = d2B[r];
-                Jr[NH - 1] = c * y0 + s_ * y1;
-                tB[r] = -s_ * y0 + c * y1;
-            }
-            __syncthreads();
-            if (h == 1) {
-                Jr[0] = tB[r];
+                for (int b = 0; b < NH - 1; b += 8) {
+                    if (live_blk(base + b, base + b + 7)) {
 #pragma unroll
-                for (int j = 0; j < NH - 1; ++j) {
-                    const double c = rot[2 * (NH + j)], s_ = rot[2 * (NH + j) + 1];
-                    const double y0 = Jr[j], y1 = Jr[j + 1];
-                    Jr[j] = c * y0 + s_ * y1;
-                    Jr[j + 1] = -s_ * y0 + c * y1;
+                        for (int j = b; j < b + 8 && j < NH - 1; ++j) {
+                            const double c = rot[2 * (base + j)], s_ = rot[2 * (base + j) + 1];
+                            const double y0 = Jr[j], y1 = Jr[j + 1];
+                            Jr[j] = c * y0 + s_ * y1;
+                            Jr[j + 1] = -s_ * y0 + c * y1;
+                        }
+                    }
                 }
+            };
+            const bool cross = !MPCQP_WG_SKIP || (jlo <= NH - 1 && jhi >= NH - 1);
+            if (cross && h == 1) d2B[r] = Jr[0];
+            __syncthreads();  // wave 0's rotations (and the carried column) are in LDS
+            if (h == 0) rot_half(0);
+            if (cross) {
+                if (h == 0) {
+                    const double c = rot[2 * (NH - 1)], s_ = rot[2 * (NH - 1) + 1];
+                    const double y0 = Jr[NH - 1], y1 = d2B[r];
+                    Jr[NH - 1] = c * y0 + s_ * y1;
+                    tB[r] = -s_ * y0 + c * y1;
+                }
+                __syncthreads();
+                if (h == 1) Jr[0] = tB[r];
             }
+            if (h == 1) rot_half(NH);
         }
         __syncthreads();
     }

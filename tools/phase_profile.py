@@ -17,7 +17,7 @@ import numpy as np  # noqa: E402
 NAMES = ["setup", "Phi/xf chains", "Qe", "H_FF", "gradient", "Cholesky", "J=L^-T",
          "unconstrained min", "dual loop", "write", "model build", "expm",
          "  sub 12 (wg: selection, J-row publication)", "  sub 13 (wg: z = J2 d2, |d|^2)",
-         "  sub 14 (wg: R solve, t1, barrier)", "  sub 15 (wg: step, add/drop, J update)"]
+         "  sub 14 (wg: r = R^-1 d, t1, barrier)", "  sub 15 (wg: step, add/drop, J update)"]
 
 
 def main():
