@@ -119,6 +119,13 @@ __device__ __forceinline__ void wg_pick(const double *red, int o, double &v, int
 #ifndef MPCQP_WG_SKIP
 #define MPCQP_WG_SKIP 1
 #endif
+// 1: a drop's rotations all at once (rotation j's hypotenuse is sqrt(R^-1(k,k)^2 + the prefix
+// sum of R^-1(k, k+1 .. j+1)^2), then each lane carries its row through the columns with the
+// column loads issued four at a time; 0: one rotation after the other, an LDS round trip and a
+// sqrt / divide on the chain per column
+#ifndef MPCQP_WG_PDROP
+#define MPCQP_WG_PDROP 1
+#endif
 
 template <int NF>
 __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double g, double *W) {
@@ -563,7 +570,84 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
                 if (ln >= k && ln < q) { us[ln] = un0; acts[ln] = an0; }
                 if (TWO && ln + 64 >= k && ln + 64 < q) { us[ln + 64] = un1; acts[ln + 64] = an1; }
                 if (ln == 0) L.st[dropped] = 1;
-                if (MPCQP_WG_RINV) {
+                if (MPCQP_WG_RINV && MPCQP_WG_PDROP) {
+                    const int qn = q - 1;
+                    const double ra0 = Lc[lrow(k) + k];
+                    const int j0 = ln, j1 = ln + 64;
+                    const double rb0 = (j0 >= k && j0 < qn) ? Lc[lrow(j0 + 1) + k] : 0.0;
+                    const double rb1 = (TWO && j1 >= k && j1 < qn) ? Lc[lrow(j1 + 1) + k] : 0.0;
+                    // the DPP moves run with every lane active: pinned here, not sunk into the
+                    // selects' branches (a disabled source lane reads 0)
+                    const double a2 = ra0 * ra0;
+                    double p0 = wave_prefix_sum(rb0 * rb0);
+                    pin(p0);
+                    const double H0 = sqrt(a2 + p0);
+                    double hp0 = wave_prev(H0);
+                    pin(hp0);
+                    if (j0 < NF) {
+                        const bool on = j0 >= k && j0 < qn;
+                        const double pv = (j0 == k) ? ra0 : hp0;
+                        const double ih = 1.0 / H0;
+                        rot[2 * j0] = on ? rb0 * ih : 1.0;
+                        rot[2 * j0 + 1] = on ? -pv * ih : 0.0;
+                    }
+                    if constexpr (TWO) {
+                        double p1 = wave_prefix_sum(rb1 * rb1);
+                        pin(p1);
+                        const double H1 = sqrt(a2 + (p1 + readlane(p0, 63)));
+                        double pw = wave_prev(H1);
+                        pin(pw);
+                        const double pv = (j1 == k) ? ra0 : (ln == 0 ? readlane(H0, 63) : pw);
+                        const bool on = j1 >= k && j1 < qn;
+                        const double ih = 1.0 / H1;
+                        if (j1 < NF) {
+                            rot[2 * j1] = on ? rb1 * ih : 1.0;
+                            rot[2 * j1 + 1] = on ? -pv * ih : 0.0;
+                        }
+                    }
+                    wave_sync();
+                    // rows ln (and ln + 64): the rotated column j (row k deleted) is final once
+                    // rotated; the carry is column j + 1 as rotated so far
+                    double cr0 = (ln <= k) ? Lc[lrow(k) + ln] : 0.0;
+                    double cr1 = (TWO && ln + 64 <= k) ? Lc[lrow(k) + ln + 64] : 0.0;
+                    auto step = [&](int j, double c, double s_, double y0, double y1) {
+                        const double o0 = c * cr0 + s_ * y0;
+                        cr0 = -s_ * cr0 + c * y0;
+                        if (ln <= j + 1 && ln != k) Lc[lrow(j) + ln - (ln > k ? 1 : 0)] = o0;
+                        if constexpr (TWO) {
+                            const int i1 = ln + 64;
+                            const double o1 = c * cr1 + s_ * y1;
+                            cr1 = -s_ * cr1 + c * y1;
+                            if (i1 <= j + 1 && i1 != k) Lc[lrow(j) + i1 - (i1 > k ? 1 : 0)] = o1;
+                        }
+                    };
+                    int j = k;
+                    // every load of a block (columns j+1 .. j+4, original) before its stores
+                    // (columns j .. j+3, rows shifted up past k): other lanes' stores land on
+                    // rows this lane reads
+                    for (; j + 4 <= qn; j += 4) {
+                        double c[4], s4[4], y0[4], y1[4];
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            c[t] = rot[2 * (j + t)];
+                            s4[t] = rot[2 * (j + t) + 1];
+                            y0[t] = (ln <= j + t + 1) ? Lc[lrow(j + t + 1) + ln] : 0.0;
+                            y1[t] = (TWO && ln + 64 <= j + t + 1) ? Lc[lrow(j + t + 1) + ln + 64] : 0.0;
+                        }
+                        step_fence();
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) step(j + t, c[t], s4[t], y0[t], y1[t]);
+                        step_fence();
+                    }
+                    for (; j < qn; ++j) {
+                        const double c = rot[2 * j], s_ = rot[2 * j + 1];
+                        const double y0 = (ln <= j + 1) ? Lc[lrow(j + 1) + ln] : 0.0;
+                        const double y1 = (TWO && ln + 64 <= j + 1) ? Lc[lrow(j + 1) + ln + 64] : 0.0;
+                        step_fence();
+                        step(j, c, s_, y0, y1);
+                        step_fence();
+                    }
+                } else if (MPCQP_WG_RINV) {
                     // R^-1 G' with the rotations that zero row k of R^-1 left of column q-1 (the
                     // same G as restores R without column k: mpc_pair.hpp), row k deleted and the
                     // last column dropped; each rotated column j is final once rotated

@@ -86,6 +86,19 @@ __device__ __forceinline__ double wave_suffix_sum(double v) {
     return v + add;
 }
 
+// inclusive prefix sum over the wave: lane l gets sum_{i <= l} v_i.  row_shr 1,2,4,8 scans each
+// 16-lane row; the rows before this one are added from their totals (lanes 15, 31, 47)
+__device__ __forceinline__ double wave_prefix_sum(double v) {
+    v += dpp_z<0x111>(v);
+    v += dpp_z<0x112>(v);
+    v += dpp_z<0x114>(v);
+    v += dpp_z<0x118>(v);
+    const double r0 = readlane(v, 15), r1 = readlane(v, 31), r2 = readlane(v, 47);
+    const int row = lane() >> 4;
+    const double add = ((row >= 1 ? r0 : 0.0) + (row >= 2 ? r1 : 0.0)) + (row >= 3 ? r2 : 0.0);
+    return v + add;
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
     v += dpp<kDppXor1>(v);
     v += dpp<kDppXor2>(v);
