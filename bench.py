@@ -7,9 +7,10 @@ support) in `config.per_config` (N = 1 only).
 
 One step = one pass of the hot path over the rank's shard, inputs resident in HBM:
   k_mpc_pair (linearise + discretise + condense + Goldfarb-Idnani solve, fused, two QPs per
-  wavefront) -> k_select_min (per-rank selection record [min key | winner's U]); `--select
-  fused` times mpcqp_batch_solve_select instead (the record built by the solve kernels' last
-  workgroup, no selection launch: measured 0.465 vs 0.462 ms per step)
+  wavefront) -> k_mpc_wg (the overflow list's instances; empty for the alternating gait) whose
+  last workgroup writes the per-rank selection record [min key | winner's U]
+  (mpcqp_batch_solve_select, the default `--select fused`: 0.376 vs 0.383 ms per step at
+  65,536, 69 vs 76 us at 4,096; `--select separate` adds the k_select_min launch instead)
   -> [N>1] ONE RCCL all-gather of the records (8 + 480 B per rank) -> k_reduce_records.
 No host synchronisation inside the step.
 
@@ -391,7 +392,7 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip the per-kernel timing pass after the timed steps")
     ap.add_argument("--selection-dry-run", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--select", choices=("fused", "separate"), default="separate",
+    ap.add_argument("--select", choices=("fused", "separate"), default="fused",
                     help="selection record from the solve kernels (fused) or k_select_min")
     args = ap.parse_args()
     fused = args.select == "fused"

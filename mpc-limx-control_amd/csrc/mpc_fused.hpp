@@ -101,9 +101,11 @@ constexpr int kSelWords = (kSelSlots + kSelTickets + 1) * kSelStride;
 // the previous launch: release / acquire at agent scope around the ticket) into the record and
 // re-arms slots and ticket for the next call on the stream.
 // scratch: 24 words of the caller's (dead) dynamic LDS, used only by a finalizing launch -- a
-// static __shared__ here would add to every kernel's LDS and cost the one-QP kernel a wave per CU
+// static __shared__ here would add to every kernel's LDS and cost the one-QP kernel a wave per CU.
+// groups: the workgroups 0 .. groups-1 that commit in a finalizing launch (the others must not
+// call; default the whole grid)
 __device__ __forceinline__ void sel_commit(const MpcArgs &a, unsigned long long k, int nV,
-                                           bool wrote, unsigned long long *scratch) {
+                                           bool wrote, unsigned long long *scratch, int groups = -1) {
     const int tid = (int)threadIdx.x, nt = (int)blockDim.x;
     int &sel_last = *reinterpret_cast<int *>(scratch + 16);
     unsigned long long *sel_red = scratch;
@@ -127,7 +129,7 @@ __device__ __forceinline__ void sel_commit(const MpcArgs &a, unsigned long long 
         // workgroup that stored instances in this launch pays for one)
         if (wrote) __threadfence();
         // relaxed RMWs: acq_rel ones at agent scope would write L2 back in every workgroup
-        const int g = (int)gridDim.x, w = (int)(blockIdx.x % kSelTickets);
+        const int g = groups > 0 ? groups : (int)gridDim.x, w = (int)(blockIdx.x % kSelTickets);
         const int words = g < kSelTickets ? g : kSelTickets;
         const unsigned need = (unsigned)((g - w + kSelTickets - 1) / kSelTickets);
         const unsigned t = __hip_atomic_fetch_add(tword(w), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

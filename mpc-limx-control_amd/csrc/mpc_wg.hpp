@@ -170,7 +170,11 @@ __device__ __forceinline__ void wg_mpc_grid(const MpcArgs &a, int *list, int *re
     if (a.sel) {
         // fused selection (list mode: the launch after the one-wave kernel): thread 0 reads
         // back the keys of the block's instances (its own stores, gi_write_wg) once the solves
-        // are done; the solves' LDS is dead, the finalizer's scratch
+        // are done; the solves' LDS is dead, the finalizer's scratch.  Only the workgroups that
+        // had an instance take a ticket (workgroup 0 alone when the list is empty: the usual
+        // case, where the launch is then little more than its dispatch)
+        const int groups = count <= 0 ? 1 : (count < (int)gridDim.x ? count : (int)gridDim.x);
+        if ((int)blockIdx.x >= groups) return;
         unsigned long long kmin = kSelNone;
         for (int i = blockIdx.x; i < count; i += gridDim.x) {
             const int b = ov.id(i);
@@ -178,7 +182,7 @@ __device__ __forceinline__ void wg_mpc_grid(const MpcArgs &a, int *list, int *re
             kmin = k < kmin ? k : kmin;
         }
         sel_commit(a, kmin, NU * N, (int)blockIdx.x < count,
-                   reinterpret_cast<unsigned long long *>(smem));
+                   reinterpret_cast<unsigned long long *>(smem), groups);
     }
 }
 

@@ -4,6 +4,7 @@
 For each batch size: median over --reps of
   * solve     : mpcqp_batch_solve, HIP events on the ctx stream (k_mpc_pair [+ k_mpc_wg])
   * step      : solve + k_select_min record, torch events (what bench.py's step is at N = 1)
+  * fused step: mpcqp_batch_solve_select (the record built by the solve kernels, bench --select fused)
 and the mean / max solver passes.  With MPCQP_LIB pointing at libmpcqp_stamps.so it also
 prints the per-WAVE cycles of each phase (s_memtime, summed over the wave's phases), which at
 small batches is the latency of a lone wavefront.
@@ -51,7 +52,7 @@ def main():
             eng.solve(d)
             eng.select_record(d, rec)
         eng.sync()
-        ks, ss = [], []
+        ks, ss, fs = [], [], []
         st = torch.cuda.current_stream()
         for _ in range(args.reps):  # solve and step, torch events (no library events inside)
             e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
@@ -63,6 +64,12 @@ def main():
             e2.synchronize()
             ks.append(e0.elapsed_time(e1))
             ss.append(e0.elapsed_time(e2))
+            e3, e4 = (torch.cuda.Event(enable_timing=True) for _ in range(2))
+            e3.record(st)
+            eng.solve_select(d, rec)  # fused: the record from the solve kernels' last workgroup
+            e4.record(st)
+            e4.synchronize()
+            fs.append(e3.elapsed_time(e4))
         # the one-wave kernel alone (library events around its launch), a separate pass
         eng.enable_timing(True)
         for _ in range(min(args.reps, 60)):
@@ -73,7 +80,7 @@ def main():
         it = d["iters"].cpu().numpy()
         stt = d["status"].cpu().numpy()
         line = (f"B {B:6d} kernel {kms / max(1, kn) * 1e3:7.1f} us solve {np.median(ks) * 1e3:7.1f} us"
-                f"  step {np.median(ss) * 1e3:7.1f} us"
+                f"  step {np.median(ss) * 1e3:7.1f} us  fused step {np.median(fs) * 1e3:7.1f} us"
                 f"  ({B / np.median(ss) / 1e3:7.2f} M QP/s)  iters mean {it.mean():.2f} max "
                 f"{it.max():3d} solved {np.mean(stt == 0):.3f}")
         if stamps:
