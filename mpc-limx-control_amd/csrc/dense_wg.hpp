@@ -22,6 +22,17 @@
 // The H rows reach the solver's registers through 16-row tiles of M = [Y_0; ..; Y_{N-1}] Phi
 // staged in LDS (H(r, c) = 2 M(r, (k_r - k_c) NU + c mod NU)), so no NV x NV matrix is ever
 // stored.  Per instance: [Ac | Bc] (NX x NS), x0, xref in; U, cost, status, iterations out.
+//
+// TOEP (Q = F_Q F_Q', P = F_P F_P' factored on the host at context creation, mpcqp_ctx_create):
+// the recursion's 16 dependent steps are replaced by one product with no chain,
+//   H = 2 (G' G + R),  G = blockdiag(F_Q', .., F_Q', F_P') Bbar,  Bbar(m, j) = Phi_{m-1-j}
+// (block lower-triangular Toeplitz), i.e. H(i, j) = 2 sum_{mb >= max(i_b, j_b)}
+// Psi(mb)_{mb-i_b}' Psi(mb)_{mb-j_b} with Psi_a = F' Phi_a: the 16 x 16 output tiles of H's
+// lower triangle run their K = NX (N - mb0) loops on the matrix cores straight out of the two
+// NX x NV Psi panels (the Toeplitz map is an address offset per lane), two row tiles per round
+// (7 tiles over the 4 waves).  The gradient takes the same panels: with E = [e_1 .. e_N]
+// (e_m = Ad^m x0 - xref_m; Ad^m x0 rides along the Phi doubling as extra columns),
+// Gamma = Psi' F' E and f_(i_b, c) = 2 sum_{mb >= i_b} Gamma((mb - i_b) NU + c, mb).
 #pragma once
 #include "condense.hpp"
 #include "expm_wg.hpp"
@@ -31,7 +42,7 @@
 
 namespace mpcqp {
 
-template <int NX, int NU, int N>
+template <int NX, int NU, int N, bool TOEP = false>
 struct DenseLayout {
     static constexpr int NS = NX + NU, NV = NU * N, NF = NV;
     static constexpr int RW = WgShape<NF>::RW;
@@ -47,7 +58,8 @@ struct DenseLayout {
     static constexpr int oX0 = oAB + NX * NS;
     static constexpr int oXr = oX0 + NX;
     static constexpr int oF = oXr + NX * (N + 1);
-    static constexpr int oR = (oF + NV + 1) & ~1;
+    static constexpr int oRm = oF + NV;                  // R, NU x NU (the H rows' diagonal blocks)
+    static constexpr int oR = (oRm + NU * NU + 1) & ~1;
     //   discretisation view
     static constexpr int oT = oR;                       // [Ac | Bc] Ts
     static constexpr int oWs = oT + NX * NS;            // wave_expm scratch (7 NX NS)
@@ -58,8 +70,21 @@ struct DenseLayout {
     static constexpr int oY = oPw + 3 * LD * NX;        // Y stack, NV x NX (ld LY)
     static constexpr int oXf = oY + LY * NX;            // e_m = Ad^m x0 - xref_m, NX x (N+1)
     static constexpr int oSv = oXf + NX * (N + 1);      // s_i, NX x N
-    static constexpr int nCond = oSv + NX * N - oR;
+    static constexpr int nCondR = oSv + NX * N - oR;
     static_assert(LS * NV <= 3 * LD * NX, "the staged M tile fits the Z region");
+    //   Toeplitz condensing view: [Phi | X] (X_a = Ad^(a+1) x0, then e_(a+1)), Psi = F_Q' [Phi | E],
+    //   Psi_P = F_P' [Phi | e_N]; Gamma and the H staging reuse the [Phi | X] panel once Psi is in
+    static constexpr int NC = NV + N;
+    static constexpr int oPx = oR;
+    static constexpr int oPs = oPx + LD * NC;
+    static constexpr int oPp = oPs + LD * NC;
+    static constexpr int LG = NV + 1;                   // Gamma, NV x N
+    static constexpr int nCondT = oPp + LD * (NV + 1) - oR;
+    static constexpr int TR = (NV + 15) / 16;           // row tiles of H
+    static_assert(LG * N <= LD * NC, "Gamma fits the [Phi | X] panel");
+    static_assert(LS * 16 * (TR + 1) <= LD * NC, "two staged row tiles fit the [Phi | X] panel");
+    static_assert(!TOEP || NX % 4 == 0, "K steps of 4 per Psi block");
+    static constexpr int nCond = TOEP ? nCondT : nCondR;
     static constexpr int nFront = oR - oU + (nExpm > nCond ? nExpm : nCond);
     // solver view (after every thread holds its H_FF row part and g)
     static constexpr int nSolver = WgLayout<NF>::work;
@@ -69,9 +94,66 @@ struct DenseLayout {
     static constexpr size_t lds_bytes = (bytes + 15) & ~(size_t)15;
 };
 
-template <int NX, int NU, int N>
+// One 16 x 16 tile (I, J), J <= I, of G' G (TOEP): lane li's A row i = 16 I + li and B column
+// j = 16 J + li take block mb's K = NX slice from Psi(mb) at Psi_{mb - i_b}(:, c_i) -- a per-lane
+// offset -- and read 0 where mb < i_b (j_b); mb starts at the tile's first row block (i >= j).
+// 1: block mb + 1's operands are loaded while block mb's MFMAs run, and even / odd K steps
+// go to two accumulators (measured 1.5 % slower at config E, 16,384: off)
+#ifndef MPCQP_TOEP_PIPE
+#define MPCQP_TOEP_PIPE 0
+#endif
+template <int NX, int NU, int N, int LD>
+__device__ __forceinline__ dx4 toep_tile(const double *Ps, const double *Pp, int I, int J) {
+    constexpr int NV = NU * N, KS = NX / 4;
+    const int ln = lane(), li = ln & 15, lk = ln >> 4;
+    const int i = 16 * I + li, j = 16 * J + li;
+    const int ib = i < NV ? i / NU : N, jb = j < NV ? j / NU : N;
+    const int offa = (i % NU - ib * NU) * LD + lk, offb = (j % NU - jb * NU) * LD + lk;
+    const int mb0 = (16 * I) / NU;
+    auto load = [&](int mb, double (&av)[KS], double (&bv)[KS]) {
+        const double *P = (mb == N - 1 ? Pp : Ps) + mb * NU * LD;
+        const bool va = mb >= ib, vb = mb >= jb;
+        const double *pa = P + (va ? offa : lk), *pb = P + (vb ? offb : lk);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const double x = pa[4 * s], y = pb[4 * s];
+            av[s] = va ? x : 0.0;
+            bv[s] = vb ? y : 0.0;
+        }
+    };
+    dx4 acc = {0.0, 0.0, 0.0, 0.0};
+    if (MPCQP_TOEP_PIPE) {
+        dx4 acc1 = {0.0, 0.0, 0.0, 0.0};
+        double av[KS], bv[KS];
+        load(mb0, av, bv);
+        for (int mb = mb0; mb < N; ++mb) {
+            double an[KS], bn[KS];
+            load(mb + 1 < N ? mb + 1 : mb, an, bn);  // (the last block's re-read is discarded)
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                if (s & 1) acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc1, 0, 0, 0);
+                else acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                av[s] = an[s];
+                bv[s] = bn[s];
+            }
+        }
+        return acc + acc1;
+    }
+    for (int mb = mb0; mb < N; ++mb) {
+        double av[KS], bv[KS];
+        load(mb, av, bv);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
+    }
+    return acc;
+}
+
+template <int NX, int NU, int N, bool TOEP = false>
 __device__ __forceinline__ void dense_mpc_one(const MpcArgs &a, int b, unsigned char *smem) {
-    using Lay = DenseLayout<NX, NU, N>;
+    using Lay = DenseLayout<NX, NU, N, TOEP>;
     constexpr int NS = Lay::NS, NV = Lay::NV, NF = Lay::NF, RW = Lay::RW, NH = NF / 2;
     constexpr int LD = Lay::LD, LY = Lay::LY, LS = Lay::LS, NT = 2 * RW;
     const WgIds T = wg_ids<RW>();
@@ -118,6 +200,7 @@ __device__ __forceinline__ void dense_mpc_one(const MpcArgs &a, int b, unsigned 
         for (int e = tid; e < NX; e += NT) x0[e] = a.x0[(size_t)b * NX + e];
         const double *xrg = a.xref + (size_t)b * NX * (N + 1);
         for (int e = tid; e < NX * (N + 1); e += NT) xr[e] = xrg[e];
+        for (int e = tid; e < NU * NU; e += NT) D[Lay::oRm + e] = a.rmat[e];
     }
     __syncthreads();
     // ---- discretisation (the workgroup, matrix cores) and the free map / bounds (wave 0)
@@ -133,129 +216,232 @@ __device__ __forceinline__ void dense_mpc_one(const MpcArgs &a, int b, unsigned 
     __syncthreads();
     MPCQP_STAMP(a.stamps, 11, tst);
 
-    // ---- Phi_a = Ad^a Bd, a = 0..N-1, by doubling: Phi[p .. p+nb) = Ad^p Phi[0 .. nb)
-    double *Phi = D + Lay::oPhi, *Pw0 = D + Lay::oPw, *Pw1 = Pw0 + LD * NX, *Pw2 = Pw1 + LD * NX;
-    for (int e = tid; e < NX * NU; e += NT) Phi[(e / NX) * LD + e % NX] = Bd[e];
-    __syncthreads();
-    {
-        const double *pw = Ad;
-        int ldp = NX;
-        double *nxt = Pw0, *oth = Pw1;
-        for (int p2 = 1; p2 < N; p2 *= 2) {
-            const int nb = p2 < N - p2 ? p2 : N - p2;
-            const bool more = 2 * p2 < N;
-            mfma_gemm<false>(NX, nb * NU, NX, pw, ldp, Phi, LD, Phi + p2 * NU * LD, LD, nullptr, 0,
-                             1.0, wv, 0, more ? 2 : 4);
-            if (more)
-                mfma_gemm<false>(NX, NX, NX, pw, ldp, pw, ldp, nxt, LD, nullptr, 0, 1.0, wv, 2, 2);
-            __syncthreads();
-            if (more) {
-                pw = nxt;
-                ldp = LD;
-                double *t_ = nxt;
-                nxt = oth;
-                oth = t_;
-            }
-        }
-    }
-    // ---- Z_{N-1} = P, Z_i = Q + Ad' Z_{i+1} Ad;  Y_i = Bd' Z_i into the stack's rows i NU ..
-    double *Y = D + Lay::oY;
-    for (int e = tid; e < NX * NX; e += NT) Pw0[(e / NX) * LD + e % NX] = a.pm[e];
-    __syncthreads();
-    {
-        double *Zc = Pw0, *Zn = Pw1;
-        for (int i = N - 1; i >= 0; --i) {
-            mfma_gemm<true>(NU, NX, NX, Bd, NX, Zc, LD, Y + i * NU, LY, nullptr, 0, 1.0, wv, 0, 2);
-            if (i > 0)
-                mfma_gemm<false>(NX, NX, NX, Zc, LD, Ad, NX, Pw2, LD, nullptr, 0, 1.0, wv, 2, 2);
-            __syncthreads();
-            if (i > 0) {
-                mfma_gemm<true>(NX, NX, NX, Ad, NX, Pw2, LD, Zn, LD, a.qm, NX, 1.0, wv, 0, 4);
-                __syncthreads();
-                double *t_ = Zc;
-                Zc = Zn;
-                Zn = t_;
-            }
-        }
-    }
-    MPCQP_STAMP(a.stamps, 1, tst);
-    // ---- gradient (wave 0): e_m = Ad^m x0 - xref_m, s_{N-1} = P e_N,
-    //      s_i = Q e_{i+1} + Ad' s_{i+1}, f_i = 2 Bd' s_i
-    if (wv == 0) {
-        double *xf = D + Lay::oXf, *sv = D + Lay::oSv;
-        if (ln < NX) xf[ln] = x0[ln];
-        wave_sync();
-        for (int m = 1; m <= N; ++m) {
-            if (ln < NX) {
-                double s = 0.0;
-#pragma unroll
-                for (int l = 0; l < NX; ++l) s += Ad[l * NX + ln] * xf[(m - 1) * NX + l];
-                xf[m * NX + ln] = s;
-            }
-            wave_sync();
-        }
-        for (int e = ln; e < NX * N; e += kWave) xf[NX + e] -= xr[NX + e];
-        wave_sync();
-        for (int i = N - 1; i >= 0; --i) {
-            if (ln < NX) {
-                const double *W = (i + 1 < N) ? a.qm : a.pm;
-                double s = 0.0;
-#pragma unroll
-                for (int l = 0; l < NX; ++l) s += W[l * NX + ln] * xf[(i + 1) * NX + l];
-                if (i + 1 < N) {
-#pragma unroll
-                    for (int l = 0; l < NX; ++l) s += Ad[ln * NX + l] * sv[(i + 1) * NX + l];
-                }
-                sv[i * NX + ln] = s;
-            }
-            wave_sync();
-        }
-        for (int e = ln; e < NV; e += kWave) {
-            const int i = e / NU, c = e % NU;
-            double s = 0.0;
-#pragma unroll
-            for (int l = 0; l < NX; ++l) s += Bd[c * NX + l] * sv[i * NX + l];
-            fv[e] = 2.0 * s;
-        }
-    }
-    __syncthreads();
-    C.nf = (int)D[Lay::oMisc];
-    C.status = (int)D[Lay::oMisc + 1];
-    C.nfric = 0;
-    C.mt = 2 * C.nf;
-    C.c0 = 0.0;
-    const int nf = C.nf;
-    const bool ok = C.status == ST_OK && nf > 0;
-    MPCQP_STAMP(a.stamps, 4, tst);
-
-    // ---- H rows: 16-row tiles of M = Y Phi staged over the Z region; thread (r, h) takes
-    //      H(r, c) = 2 (M(r, (k_r - k_c) NU + c mod NU) + R(c_r, c_c) [k_r == k_c]), c = 2j + h
-    //      <= r (gi_run_wg's interleaved factorisation layout; identity beyond nf)
     double hr[NH];
 #pragma unroll
     for (int j = 0; j < NH; ++j) hr[j] = (r == 2 * j + h) ? 1.0 : 0.0;
-    double *stg = Pw0;
-    for (int r0 = 0; r0 < NV; r0 += 16) {
-        const int nrow = NV - r0 < 16 ? NV - r0 : 16;
-        const int ncol = ((r0 + nrow - 1) / NU + 1) * NU;  // columns a NU + c with a <= k_r
-        mfma_gemm<false, false>(nrow, ncol, NX, Y + r0, LY, Phi, LD, stg, LS, nullptr, 0, 1.0, wv, 0, 4);
+    int nf = 0;
+    bool ok = false;
+    if constexpr (TOEP) {
+        // ---- [Phi | X]: Phi_a = Ad^a Bd and X_a = Ad^(a+1) x0, a = 0..N-1, by doubling
+        constexpr int NC = Lay::NC;
+        double *Px = D + Lay::oPx, *Ps = D + Lay::oPs, *Pp = D + Lay::oPp;
+        double *Pw0 = Ps, *Pw1 = Ps + LD * NX;  // the powers of Ad, in the (not yet written) Psi
+        for (int e = tid; e < NX * NU; e += NT) Px[(e / NX) * LD + e % NX] = Bd[e];
+        mfma_gemm<false>(NX, 1, NX, Ad, NX, x0, NX, Px + NV * LD, LD, nullptr, 0, 1.0, wv, 2, 2);
         __syncthreads();
-        if (ok && r >= r0 && r < r0 + nrow && r < nf) {
-            const int kr = r / NU, cr = r % NU;
-#pragma unroll
-            for (int j = 0; j < NH; ++j) {
-                const int c = 2 * j + h;
-                if (c <= r) {
-                    const int kc = c / NU, cc = c % NU;
-                    double v = stg[((kr - kc) * NU + cc) * LS + (r - r0)];
-                    if (kr == kc) v += a.rmat[cc * NU + cr];
-                    hr[j] = 2.0 * v;
+        {
+            const double *pw = Ad;
+            int ldp = NX;
+            double *nxt = Pw0, *oth = Pw1;
+            for (int p2 = 1; p2 < N; p2 *= 2) {
+                const int nb = p2 < N - p2 ? p2 : N - p2;
+                const bool more = 2 * p2 < N;
+                mfma_gemm<false>(NX, nb * NU, NX, pw, ldp, Px, LD, Px + p2 * NU * LD, LD, nullptr, 0,
+                                 1.0, wv, 0, 4);
+                mfma_gemm<false>(NX, nb, NX, pw, ldp, Px + NV * LD, LD, Px + (NV + p2) * LD, LD,
+                                 nullptr, 0, 1.0, wv, 2, 2);
+                if (more)
+                    mfma_gemm<false>(NX, NX, NX, pw, ldp, pw, ldp, nxt, LD, nullptr, 0, 1.0, wv, 0, 4);
+                __syncthreads();
+                if (more) {
+                    pw = nxt;
+                    ldp = LD;
+                    double *t_ = nxt;
+                    nxt = oth;
+                    oth = t_;
                 }
-                if ((j & 7) == 7) step_fence();
+            }
+        }
+        // e_m = Ad^m x0 - xref_m in place of X_(m-1)
+        for (int e = tid; e < NX * N; e += NT) Px[(NV + e / NX) * LD + e % NX] -= xr[NX + e];
+        __syncthreads();
+        // ---- Psi = F_Q' [Phi | E], Psi_P = F_P' [Phi | e_N] (F from global memory)
+        mfma_gemm<true>(NX, NC, NX, a.fq, NX, Px, LD, Ps, LD, nullptr, 0, 1.0, wv, 0, 4);
+        mfma_gemm<true>(NX, NV, NX, a.fp, NX, Px, LD, Pp, LD, nullptr, 0, 1.0, wv, 0, 4);
+        mfma_gemm<true>(NX, 1, NX, a.fp, NX, Px + (NC - 1) * LD, LD, Pp + NV * LD, LD, nullptr, 0,
+                        1.0, wv, 2, 2);
+        __syncthreads();
+        MPCQP_STAMP(a.stamps, 1, tst);
+        // ---- gradient: Gamma(:, mb) = Psi(mb)' w_mb (the e columns of Psi / Psi_P), then
+        //      f_(i_b, c) = 2 sum_{mb >= i_b} Gamma((mb - i_b) NU + c, mb)
+        double *G = Px;
+        constexpr int LG = Lay::LG;
+        mfma_gemm<true>(NV, N - 1, NX, Ps, LD, Ps + NV * LD, LD, G, LG, nullptr, 0, 1.0, wv, 0, 4);
+        mfma_gemm<true>(NV, 1, NX, Pp, LD, Pp + NV * LD, LD, G + (N - 1) * LG, LG, nullptr, 0, 1.0,
+                        wv, 0, 4);
+        __syncthreads();
+        for (int e = tid; e < NV; e += NT) {
+            const int ib = e / NU, c = e % NU;
+            double s = 0.0;
+            for (int mb = ib; mb < N; ++mb) s += G[mb * LG + (mb - ib) * NU + c];
+            fv[e] = 2.0 * s;
+        }
+        __syncthreads();
+        C.nf = (int)D[Lay::oMisc];
+        C.status = (int)D[Lay::oMisc + 1];
+        nf = C.nf;
+        ok = C.status == ST_OK && nf > 0;
+        MPCQP_STAMP(a.stamps, 4, tst);
+        // ---- H rows: rounds of two row tiles (rho, TR-1-rho): their 16 I + 16 tiles of G' G
+        //      over the waves, staged (rows of I at stg, of I' after them), then every thread
+        //      takes H(r, c) = 2 (G'G(r, c) + R(c_c, c_r) [k_r == k_c]), c = 2j + h <= r
+        constexpr int TR = Lay::TR;
+        double *stg = Px;
+        MPCQP_STAMP_INIT(th);  // diagnostic build: tiles (slot 2) and row pickup (slot 10)
+        for (int rho = 0; rho < (TR + 1) / 2; ++rho) {
+            const int Ia = rho, Ib = TR - 1 - rho;
+            const int na = Ia + 1, nt_ = Ia == Ib ? na : na + Ib + 1;
+            double *sb = stg + LS * 16 * na;
+            for (int t = wv; t < nt_; t += NT / 64) {
+                const int I = t < na ? Ia : Ib, J = t < na ? t : t - na;
+                const dx4 acc = toep_tile<NX, NU, N, LD>(Ps, Pp, I, J);
+                double *st_ = t < na ? stg : sb;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) st_[(16 * J + (ln & 15)) * LS + (ln >> 4) + 4 * q] = acc[q];
+            }
+            __syncthreads();
+            MPCQP_STAMP(a.stamps, 2, th);
+            const int Ir = r >> 4;
+            if (ok && (Ir == Ia || Ir == Ib) && r < nf) {
+                const double *st_ = Ir == Ia ? stg : sb;
+                const int kr = r / NU, cr = r % NU, rr = r & 15;
+#pragma unroll
+                for (int j = 0; j < NH; ++j) {
+                    const int c = 2 * j + h;
+                    if (c <= r) {
+                        const int kc = c / NU, cc = c % NU;
+                        double v = st_[c * LS + rr];
+                        if (kr == kc) v += D[Lay::oRm + cc * NU + cr];
+                        hr[j] = 2.0 * v;
+                    }
+                    if ((j & 7) == 7) step_fence();
+                }
+            }
+            __syncthreads();
+            MPCQP_STAMP(a.stamps, 10, th);
+        }
+    } else {
+        // ---- Phi_a = Ad^a Bd, a = 0..N-1, by doubling: Phi[p .. p+nb) = Ad^p Phi[0 .. nb)
+        double *Phi = D + Lay::oPhi, *Pw0 = D + Lay::oPw, *Pw1 = Pw0 + LD * NX, *Pw2 = Pw1 + LD * NX;
+        for (int e = tid; e < NX * NU; e += NT) Phi[(e / NX) * LD + e % NX] = Bd[e];
+        __syncthreads();
+        {
+            const double *pw = Ad;
+            int ldp = NX;
+            double *nxt = Pw0, *oth = Pw1;
+            for (int p2 = 1; p2 < N; p2 *= 2) {
+                const int nb = p2 < N - p2 ? p2 : N - p2;
+                const bool more = 2 * p2 < N;
+                mfma_gemm<false>(NX, nb * NU, NX, pw, ldp, Phi, LD, Phi + p2 * NU * LD, LD, nullptr, 0,
+                                 1.0, wv, 0, more ? 2 : 4);
+                if (more)
+                    mfma_gemm<false>(NX, NX, NX, pw, ldp, pw, ldp, nxt, LD, nullptr, 0, 1.0, wv, 2, 2);
+                __syncthreads();
+                if (more) {
+                    pw = nxt;
+                    ldp = LD;
+                    double *t_ = nxt;
+                    nxt = oth;
+                    oth = t_;
+                }
+            }
+        }
+        // ---- Z_{N-1} = P, Z_i = Q + Ad' Z_{i+1} Ad;  Y_i = Bd' Z_i into the stack's rows i NU ..
+        double *Y = D + Lay::oY;
+        for (int e = tid; e < NX * NX; e += NT) Pw0[(e / NX) * LD + e % NX] = a.pm[e];
+        __syncthreads();
+        {
+            double *Zc = Pw0, *Zn = Pw1;
+            for (int i = N - 1; i >= 0; --i) {
+                mfma_gemm<true>(NU, NX, NX, Bd, NX, Zc, LD, Y + i * NU, LY, nullptr, 0, 1.0, wv, 0, 2);
+                if (i > 0)
+                    mfma_gemm<false>(NX, NX, NX, Zc, LD, Ad, NX, Pw2, LD, nullptr, 0, 1.0, wv, 2, 2);
+                __syncthreads();
+                if (i > 0) {
+                    mfma_gemm<true>(NX, NX, NX, Ad, NX, Pw2, LD, Zn, LD, a.qm, NX, 1.0, wv, 0, 4);
+                    __syncthreads();
+                    double *t_ = Zc;
+                    Zc = Zn;
+                    Zn = t_;
+                }
+            }
+        }
+        MPCQP_STAMP(a.stamps, 1, tst);
+        // ---- gradient (wave 0): e_m = Ad^m x0 - xref_m, s_{N-1} = P e_N,
+        //      s_i = Q e_{i+1} + Ad' s_{i+1}, f_i = 2 Bd' s_i
+        if (wv == 0) {
+            double *xf = D + Lay::oXf, *sv = D + Lay::oSv;
+            if (ln < NX) xf[ln] = x0[ln];
+            wave_sync();
+            for (int m = 1; m <= N; ++m) {
+                if (ln < NX) {
+                    double s = 0.0;
+#pragma unroll
+                    for (int l = 0; l < NX; ++l) s += Ad[l * NX + ln] * xf[(m - 1) * NX + l];
+                    xf[m * NX + ln] = s;
+                }
+                wave_sync();
+            }
+            for (int e = ln; e < NX * N; e += kWave) xf[NX + e] -= xr[NX + e];
+            wave_sync();
+            for (int i = N - 1; i >= 0; --i) {
+                if (ln < NX) {
+                    const double *W = (i + 1 < N) ? a.qm : a.pm;
+                    double s = 0.0;
+#pragma unroll
+                    for (int l = 0; l < NX; ++l) s += W[l * NX + ln] * xf[(i + 1) * NX + l];
+                    if (i + 1 < N) {
+#pragma unroll
+                        for (int l = 0; l < NX; ++l) s += Ad[ln * NX + l] * sv[(i + 1) * NX + l];
+                    }
+                    sv[i * NX + ln] = s;
+                }
+                wave_sync();
+            }
+            for (int e = ln; e < NV; e += kWave) {
+                const int i = e / NU, c = e % NU;
+                double s = 0.0;
+#pragma unroll
+                for (int l = 0; l < NX; ++l) s += Bd[c * NX + l] * sv[i * NX + l];
+                fv[e] = 2.0 * s;
             }
         }
         __syncthreads();
+        C.nf = (int)D[Lay::oMisc];
+        C.status = (int)D[Lay::oMisc + 1];
+        nf = C.nf;
+        ok = C.status == ST_OK && nf > 0;
+        MPCQP_STAMP(a.stamps, 4, tst);
+
+        // ---- H rows: 16-row tiles of M = Y Phi staged over the Z region; thread (r, h) takes
+        //      H(r, c) = 2 (M(r, (k_r - k_c) NU + c mod NU) + R(c_r, c_c) [k_r == k_c]), c = 2j + h
+        //      <= r (gi_run_wg's interleaved factorisation layout; identity beyond nf)
+        double *stg = Pw0;
+        for (int r0 = 0; r0 < NV; r0 += 16) {
+            const int nrow = NV - r0 < 16 ? NV - r0 : 16;
+            const int ncol = ((r0 + nrow - 1) / NU + 1) * NU;  // columns a NU + c with a <= k_r
+            mfma_gemm<false, false>(nrow, ncol, NX, Y + r0, LY, Phi, LD, stg, LS, nullptr, 0, 1.0, wv, 0, 4);
+            __syncthreads();
+            if (ok && r >= r0 && r < r0 + nrow && r < nf) {
+                const int kr = r / NU, cr = r % NU;
+#pragma unroll
+                for (int j = 0; j < NH; ++j) {
+                    const int c = 2 * j + h;
+                    if (c <= r) {
+                        const int kc = c / NU, cc = c % NU;
+                        double v = stg[((kr - kc) * NU + cc) * LS + (r - r0)];
+                        if (kr == kc) v += a.rmat[cc * NU + cr];
+                        hr[j] = 2.0 * v;
+                    }
+                    if ((j & 7) == 7) step_fence();
+                }
+            }
+            __syncthreads();
+        }
     }
+    C.nfric = 0;
+    C.mt = 2 * C.nf;
+    C.c0 = 0.0;
     const double g = (ok && r < nf) ? fv[C.L.fid[r]] : 0.0;
     __syncthreads();  // the solver's workspace overlays the front
     MPCQP_STAMP(a.stamps, 3, tst);

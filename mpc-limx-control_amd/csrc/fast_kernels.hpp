@@ -47,7 +47,9 @@ bool add_fast_pair(int model, int N, bool fric, int nfmax, FastKernels &k);
 // workgroup-per-QP kernels (fast_wg.hip) for the instances beyond the one-wave capacity
 bool add_fast_wg(int model, int N, bool fric, FastKernels &k);
 // dense-model kernels (fast_dense.hip): config E, 24/6/16
-bool pick_fast_dense(int nx, int nu, int N, FastKernels &k);
+// toep: Q and P have symmetric factors (the Toeplitz condensing, dense_wg.hpp); otherwise the
+// Riccati-style recursion
+bool pick_fast_dense(int nx, int nu, int N, bool toep, FastKernels &k);
 
 #ifdef MPCQP_FAST_TU
 namespace {

@@ -41,6 +41,7 @@ struct MpcArgs {
     double Ibinv[9];
     const double *qd, *pd;  // diagonals of Q and P (device)
     const double *qm, *pm;  // Q and P, nx x nx column-major (device; the dense model)
+    const double *fq, *fp;  // F with Q = F F', P = F F' (dense model, Toeplitz condensing)
     const double *rmat;     // R, nu x nu column-major (device)
     double fz_min, fz_max, fxy_max, u_min, u_max, mu;
     int max_iter, max_free;

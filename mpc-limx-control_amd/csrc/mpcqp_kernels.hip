@@ -530,6 +530,7 @@ struct mpcqp_ctx {
     bool fast = false;
     FastKernels fk;
     double *dqd = nullptr, *dpd = nullptr;  // diagonals of Q, P
+    double *dFQ = nullptr, *dFP = nullptr;  // dense model: Q = F F', P = F F' (sym_factor)
     double *dAB = nullptr;                  // [B][nx*(nx+nu)] discretised model scratch
     size_t ab_cap = 0;
     unsigned long long *dstamps = nullptr;  // diagnostic phase cycles (stamps build)
@@ -787,6 +788,65 @@ out:
 }
 
 // ------------------------------------------------------------------------- batched path
+// F (n x n, column-major) with M = F F' for a symmetric positive semi-definite M: the square
+// roots of a diagonal M, otherwise cyclic Jacobi M = V L V' and F = V L^(1/2).  false if M is
+// not symmetric or has an eigenvalue below -1e-12 max |eigenvalue| (the dense kernel then keeps
+// the recursion, which takes any Q and P)
+static bool sym_factor(const double *M, int n, double *F) {
+    double mx = 0.0;
+    for (int i = 0; i < n * n; ++i) mx = std::max(mx, std::fabs(M[i]));
+    for (int j = 0; j < n; ++j)
+        for (int i = 0; i < j; ++i)
+            if (std::fabs(M[j * n + i] - M[i * n + j]) > 1e-14 * mx) return false;
+    bool diag = true;
+    for (int j = 0; j < n && diag; ++j)
+        for (int i = 0; i < n; ++i)
+            if (i != j && M[j * n + i] != 0.0) { diag = false; break; }
+    std::vector<double> A(M, M + (size_t)n * n), V((size_t)n * n, 0.0);
+    for (int i = 0; i < n; ++i) V[(size_t)i * n + i] = 1.0;
+    if (!diag) {
+        for (int sweep = 0; sweep < 64; ++sweep) {
+            double off = 0.0;
+            for (int q = 0; q < n; ++q)
+                for (int p = 0; p < q; ++p) off += A[(size_t)q * n + p] * A[(size_t)q * n + p];
+            if (off <= 1e-32 * mx * mx) break;
+            for (int q = 1; q < n; ++q)
+                for (int p = 0; p < q; ++p) {
+                    const double apq = A[(size_t)q * n + p];
+                    if (apq == 0.0) continue;
+                    const double app = A[(size_t)p * n + p], aqq = A[(size_t)q * n + q];
+                    const double th = (aqq - app) / (2.0 * apq);
+                    const double t = (th >= 0 ? 1.0 : -1.0) / (std::fabs(th) + std::sqrt(th * th + 1.0));
+                    const double c = 1.0 / std::sqrt(t * t + 1.0), sn = t * c;
+                    for (int k = 0; k < n; ++k) {  // A <- J' A J, columns then rows
+                        const double akp = A[(size_t)p * n + k], akq = A[(size_t)q * n + k];
+                        A[(size_t)p * n + k] = c * akp - sn * akq;
+                        A[(size_t)q * n + k] = sn * akp + c * akq;
+                    }
+                    for (int k = 0; k < n; ++k) {
+                        const double apk = A[(size_t)k * n + p], aqk = A[(size_t)k * n + q];
+                        A[(size_t)k * n + p] = c * apk - sn * aqk;
+                        A[(size_t)k * n + q] = sn * apk + c * aqk;
+                    }
+                    for (int k = 0; k < n; ++k) {
+                        const double vkp = V[(size_t)p * n + k], vkq = V[(size_t)q * n + k];
+                        V[(size_t)p * n + k] = c * vkp - sn * vkq;
+                        V[(size_t)q * n + k] = sn * vkp + c * vkq;
+                    }
+                }
+        }
+    }
+    double lmax = 0.0;
+    for (int i = 0; i < n; ++i) lmax = std::max(lmax, std::fabs(A[(size_t)i * n + i]));
+    for (int k = 0; k < n; ++k) {
+        const double l = A[(size_t)k * n + k];
+        if (l < -1e-12 * lmax) return false;
+        const double sl = l > 0.0 ? std::sqrt(l) : 0.0;
+        for (int i = 0; i < n; ++i) F[(size_t)k * n + i] = V[(size_t)k * n + i] * sl;
+    }
+    return true;
+}
+
 static bool is_diag(const double *M, int n) {
     for (int j = 0; j < n; ++j)
         for (int i = 0; i < n; ++i)
@@ -855,9 +915,22 @@ int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
                            (m->fz_min < m->fz_max && m->fxy_max > 0.0);
     c->fast = m->model != MPCQP_MODEL_DENSE && is_diag(m->Q, nx) && is_diag(m->P, nx) &&
               bounds_ok && nu <= 6 && pick_fast(m->model, nx, nu, m->N, fric, nfmax, c->fk);
-    if (m->model == MPCQP_MODEL_DENSE && nfmax <= 128 && pick_fast_dense(nx, nu, m->N, c->fk)) {
-        c->fast = true;  // dense Q/R/P allowed: the kernel reads them whole
-        set_lds(c->fk.dense, c->fk.dense_lds);
+    if (m->model == MPCQP_MODEL_DENSE && nfmax <= 128) {
+        // dense Q/R/P allowed: the kernel reads them whole; symmetric PSD Q and P are factored
+        // for the Toeplitz condensing (dense_wg.hpp)
+        std::vector<double> fq((size_t)nx * nx), fp((size_t)nx * nx);
+        bool toep = sym_factor(m->Q, nx, fq.data()) && sym_factor(m->P, nx, fp.data());
+        if (toep && (hipMalloc(&c->dFQ, sizeof(double) * nx * nx) != hipSuccess ||
+                     hipMalloc(&c->dFP, sizeof(double) * nx * nx) != hipSuccess ||
+                     hipMemcpy(c->dFQ, fq.data(), sizeof(double) * nx * nx, hipMemcpyHostToDevice) != hipSuccess ||
+                     hipMemcpy(c->dFP, fp.data(), sizeof(double) * nx * nx, hipMemcpyHostToDevice) != hipSuccess)) {
+            mpcqp_ctx_destroy(c);
+            return MPCQP_ERR_DEVICE;
+        }
+        if (pick_fast_dense(nx, nu, m->N, toep, c->fk)) {
+            c->fast = true;
+            set_lds(c->fk.dense, c->fk.dense_lds);
+        }
     }
     if (!c->fast && nfmax > kWave) {  // the generic one-wave solver holds 64 free variables
         mpcqp_ctx_destroy(c);
@@ -914,6 +987,8 @@ int mpcqp_ctx_destroy(mpcqp_ctx *c) {
     hipFree(c->dP);
     hipFree(c->dqd);
     hipFree(c->dpd);
+    hipFree(c->dFQ);
+    hipFree(c->dFP);
     hipFree(c->dAB);
     hipFree(c->dstamps);
     hipFree(c->dsel);
@@ -1060,6 +1135,8 @@ static MpcArgs mpc_args(mpcqp_ctx *c, int B) {
     a.pd = c->dpd;
     a.qm = c->dQ;
     a.pm = c->dP;
+    a.fq = c->dFQ;
+    a.fp = c->dFP;
     a.rmat = c->dR;
     a.fz_min = m.fz_min;
     a.fz_max = m.fz_max;

@@ -14,8 +14,8 @@ sys.path.insert(0, os.path.join(ROOT, "mpc-limx-control_amd"))
 
 import numpy as np  # noqa: E402
 
-NAMES = ["setup", "Phi/xf chains", "Qe", "H_FF", "gradient", "Cholesky", "J=L^-T",
-         "unconstrained min", "dual loop", "write", "model build", "expm",
+NAMES = ["setup", "Phi/xf chains", "Qe (dense TOEP: H tiles)", "H_FF", "gradient", "Cholesky", "J=L^-T",
+         "unconstrained min", "dual loop", "write", "model build (dense TOEP: H row pickup)", "expm",
          "  sub 12 (wg: selection, J-row publication)", "  sub 13 (wg: z = J2 d2, |d|^2)",
          "  sub 14 (wg: r = R^-1 d, t1, barrier)", "  sub 15 (wg: step, add/drop, J update)"]
 
