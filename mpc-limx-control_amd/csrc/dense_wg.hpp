@@ -82,7 +82,8 @@ struct DenseLayout {
     static constexpr int nCondT = oPp + LD * (NV + 1) - oR;
     static constexpr int TR = (NV + 15) / 16;           // row tiles of H
     static_assert(LG * N <= LD * NC, "Gamma fits the [Phi | X] panel");
-    static_assert(LS * 16 * (TR + 1) <= LD * NC, "two staged row tiles fit the [Phi | X] panel");
+    static_assert(LS * 16 * (TR + 1 + 2) <= LD * NC,
+                  "two staged row tiles and two split tiles' halves fit the [Phi | X] panel");
     static_assert(!TOEP || NX % 4 == 0, "K steps of 4 per Psi block");
     static constexpr int nCond = TOEP ? nCondT : nCondR;
     static constexpr int nFront = oR - oU + (nExpm > nCond ? nExpm : nCond);
@@ -99,17 +100,22 @@ struct DenseLayout {
 // offset -- and read 0 where mb < i_b (j_b); mb starts at the tile's first row block (i >= j).
 // 1: block mb + 1's operands are loaded while block mb's MFMAs run, and even / odd K steps
 // go to two accumulators (measured 1.5 % slower at config E, 16,384: off)
+// 0: tile t of a round to wave t % 4, no K split (A/B builds)
+#ifndef MPCQP_TOEP_LPT
+#define MPCQP_TOEP_LPT 1
+#endif
 #ifndef MPCQP_TOEP_PIPE
 #define MPCQP_TOEP_PIPE 0
 #endif
 template <int NX, int NU, int N, int LD>
-__device__ __forceinline__ dx4 toep_tile(const double *Ps, const double *Pp, int I, int J) {
+__device__ __forceinline__ dx4 toep_tile(const double *Ps, const double *Pp, int I, int J, int mlo,
+                                         int mhi) {
     constexpr int NV = NU * N, KS = NX / 4;
     const int ln = lane(), li = ln & 15, lk = ln >> 4;
     const int i = 16 * I + li, j = 16 * J + li;
     const int ib = i < NV ? i / NU : N, jb = j < NV ? j / NU : N;
     const int offa = (i % NU - ib * NU) * LD + lk, offb = (j % NU - jb * NU) * LD + lk;
-    const int mb0 = (16 * I) / NU;
+    const int mb0 = mlo;
     auto load = [&](int mb, double (&av)[KS], double (&bv)[KS]) {
         const double *P = (mb == N - 1 ? Pp : Ps) + mb * NU * LD;
         const bool va = mb >= ib, vb = mb >= jb;
@@ -126,9 +132,9 @@ __device__ __forceinline__ dx4 toep_tile(const double *Ps, const double *Pp, int
         dx4 acc1 = {0.0, 0.0, 0.0, 0.0};
         double av[KS], bv[KS];
         load(mb0, av, bv);
-        for (int mb = mb0; mb < N; ++mb) {
+        for (int mb = mb0; mb < mhi; ++mb) {
             double an[KS], bn[KS];
-            load(mb + 1 < N ? mb + 1 : mb, an, bn);  // (the last block's re-read is discarded)
+            load(mb + 1 < mhi ? mb + 1 : mb, an, bn);  // (the last block's re-read is discarded)
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
                 if (s & 1) acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc1, 0, 0, 0);
@@ -142,7 +148,7 @@ __device__ __forceinline__ dx4 toep_tile(const double *Ps, const double *Pp, int
         }
         return acc + acc1;
     }
-    for (int mb = mb0; mb < N; ++mb) {
+    for (int mb = mb0; mb < mhi; ++mb) {
         double av[KS], bv[KS];
         load(mb, av, bv);
 #pragma unroll
@@ -292,14 +298,39 @@ __device__ __forceinline__ void dense_mpc_one(const MpcArgs &a, int b, unsigned 
             const int Ia = rho, Ib = TR - 1 - rho;
             const int na = Ia + 1, nt_ = Ia == Ib ? na : na + Ib + 1;
             double *sb = stg + LS * 16 * na;
-            for (int t = wv; t < nt_; t += NT / 64) {
+            // the K blocks of a tile: mb = its first row block .. N-1.  Greedy over the waves in
+            // tile order (the first row tile's K are the larger); when the first row tile's K
+            // exceeds a quarter of the round (only for <= 2 tiles: the staging room), its tiles
+            // go out as two K halves, the second half staged apart (ex) and added before pickup
+            const int Ka = N - (16 * Ia) / NU, Kb = Ia == Ib ? 0 : N - (16 * Ib) / NU;
+            const int avg = (na * Ka + (nt_ - na) * Kb + 3) / 4;
+            const bool split = MPCQP_TOEP_LPT && na <= 2 && Ka > avg;
+            double *ex = stg + LS * 16 * (Ia == Ib ? na : na + Ib + 1);
+            int l0 = 0, l1 = 0, l2 = 0, l3 = 0;  // K blocks handed to each wave so far
+            for (int t = 0; t < nt_; ++t) {
                 const int I = t < na ? Ia : Ib, J = t < na ? t : t - na;
-                const dx4 acc = toep_tile<NX, NU, N, LD>(Ps, Pp, I, J);
-                double *st_ = t < na ? stg : sb;
+                const int m0 = (16 * I) / NU, K = N - m0;
+                const int parts = (split && t < na) ? 2 : 1;
+                for (int part = 0; part < parts; ++part) {
+                    const int lo = part ? m0 + K / 2 : m0, hi = parts == 2 && !part ? m0 + K / 2 : N;
+                    const int m01 = l1 < l0 ? l1 : l0, m23 = l3 < l2 ? l3 : l2;
+                    const int w = !MPCQP_TOEP_LPT ? t % 4 : m23 < m01 ? (l3 < l2 ? 3 : 2) : (l1 < l0 ? 1 : 0);
+                    l0 += w == 0 ? hi - lo : 0;
+                    l1 += w == 1 ? hi - lo : 0;
+                    l2 += w == 2 ? hi - lo : 0;
+                    l3 += w == 3 ? hi - lo : 0;
+                    if (w != wv) continue;
+                    const dx4 acc = toep_tile<NX, NU, N, LD>(Ps, Pp, I, J, lo, hi);
+                    double *st_ = part ? ex + J * 16 * LS : (t < na ? stg : sb) + 16 * J * LS;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) st_[(16 * J + (ln & 15)) * LS + (ln >> 4) + 4 * q] = acc[q];
+                    for (int q = 0; q < 4; ++q) st_[(ln & 15) * LS + (ln >> 4) + 4 * q] = acc[q];
+                }
             }
             __syncthreads();
+            if (split) {  // the second K halves onto the first (same tile layout)
+                for (int e = tid; e < na * 16 * LS; e += NT) stg[e] += ex[e];
+                __syncthreads();
+            }
             MPCQP_STAMP(a.stamps, 2, th);
             const int Ir = r >> 4;
             if (ok && (Ir == Ia || Ir == Ib) && r < nf) {

@@ -687,6 +687,37 @@ def test_dense_fused_vs_oracle(gpu, orc):
     assert np.mean(o["iters"] == ref["iters"]) >= 0.95
 
 
+def test_dense_full_weights_vs_oracle(gpu, orc):
+    """config E with full symmetric Q and P (off-diagonal weights, Q rank-deficient PSD): the
+    host factors them by Jacobi (Q = F F') for the Toeplitz condensing; U / cost / status
+    against the oracle, which forms B'QB directly"""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("E")
+    rng = np.random.default_rng(31)
+    nx = p["nx"]
+    A = rng.standard_normal((nx, nx - 4))
+    Q = 200.0 * (A @ A.T) / nx  # full, PSD of rank nx - 4 (zero eigenvalues)
+    Bm = rng.standard_normal((nx, nx - 6))
+    P = 100.0 * (Bm @ Bm.T) / nx + np.diag(np.r_[np.zeros(6), np.diag(p["P"])[6:]])  # full, PD
+    p["Q"], p["P"] = 0.5 * (Q + Q.T), 0.5 * (P + P.T)
+    B = 128
+    batch = mpcqp.make_batch(p, B, seed=17)
+    eng = BatchEngine(p)
+    assert eng.fused_kernel == "k_dense_wg"
+    d = _prefilled(eng, batch)
+    eng.solve(d)
+    eng.sync()
+    o = {k: d[k].cpu().numpy() for k in ("U", "cost", "status", "iters")}
+    eng.close()
+    ref = orc.dense_batch(p, batch["x0"], batch["xref"], batch["lin"])
+    np.testing.assert_array_equal(o["status"], ref["status"])
+    assert np.all(ref["status"] == 0)
+    bad = [i for i in range(B) if not u_close(o["U"][i], ref["U"][i])]
+    assert not bad, bad[:10]
+    np.testing.assert_allclose(o["cost"], ref["cost"], rtol=1e-9, atol=1e-9)
+
+
 def test_dense_full_size_properties(gpu, orc):
     """config E at its BASELINE batch (16,384): all solved, deterministic, sample vs oracle"""
     import mpcqp
