@@ -120,6 +120,15 @@ __device__ __forceinline__ bool warm_bit(const unsigned long long *w, int i) {
 // lane) rather than v_readlane pairs, which cost VALU issue slots.  Fills C.{status,x,u,fval,act,q,iters}.
 // TILES: the start comes from the packed H_FF in L.R (Hb) through the blocked MFMA
 // factorisation of chol_reg.hpp instead of the column sweeps over h (h unused).
+// The dual loop keeps R^-1 (column-major packed, (i, j) at lrow(j) + i, in L.R) instead of R:
+// r = R^-1 d is a product whose loads pipeline instead of a back substitution whose every step
+// waits on the previous one; the add writes column q = (-r / r_qq, 1 / r_qq); a drop computes
+// every Givens rotation at once from a prefix sum over row k of R^-1 and each lane carries its
+// row through the columns (gi_wg.hpp, mpc_pair.hpp).  0 keeps R (A/B builds).
+#ifndef MPCQP_REG_RINV
+#define MPCQP_REG_RINV 1
+#endif
+
 template <int NF, bool TILES = false>
 __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, double *rowbuf,
                                            const WarmSet *warm = nullptr) {
@@ -370,6 +379,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         double zq = (ln > q && ln < nf) ? dj * dj : 0.0;  // |d2|^2 without d_q
         wave_sum3(dd, zn, zq);
         if (ln < NF) colb[ln] = (ln >= q) ? dj : 0.0;  // d_j = 0 for j >= nf
+        if (MPCQP_REG_RINV && ln < NF) rinv[ln] = dj;   // d (the R^-1 product reads it)
         wave_sync();
         double z4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -382,7 +392,27 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         // r = R^-1 d(0:q) (R in LDS, 1/R(j,j) kept beside it); nothing to do while q == 0
         double r = 0.0, t1 = INFINITY;
         int kslot = 0x7fffffff;
-        if (q > 0) {
+        if (MPCQP_REG_RINV && q > 0) {
+            // r_i = sum_{j = i}^{q-1} R^-1(i, j) d_j: lane i reads row i of R^-1 against the
+            // broadcast d_j; two accumulators, the loads of four columns issued together
+            double a0 = 0.0, a1 = 0.0;
+            int j = 0;
+            for (; j + 1 < q; j += 2) {
+                const double v0 = L.R[ln <= j ? lrow(j) + ln : 0], d0 = rinv[j];
+                const double v1 = L.R[ln <= j + 1 ? lrow(j + 1) + ln : 0], d1 = rinv[j + 1];
+                a0 = fma(ln <= j ? v0 : 0.0, d0, a0);
+                a1 = fma(ln <= j + 1 ? v1 : 0.0, d1, a1);
+            }
+            if (j < q) {
+                const double v0 = L.R[ln <= j ? lrow(j) + ln : 0];
+                a0 = fma(ln <= j ? v0 : 0.0, rinv[j], a0);
+            }
+            r = (ln < q) ? a0 + a1 : 0.0;
+            const double rmax = wave_max(fabs(r));
+            if (ln < q && r > kRTol * rmax) { t1 = u / r; kslot = ln; }
+            wave_argmin(t1, kslot);
+        }
+        if (!MPCQP_REG_RINV && q > 0) {
             // the chain from one step to the next is v_readlane -> mul -> FMA in registers:
             // 1/R(j,j) comes out of a register (lane j), R's columns are loaded four at a time
             // one block ahead; the FMA runs on every lane (a lane at or past its slot only
@@ -445,8 +475,16 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             }
             wave_sync();
             if (ln == q) colb[q] = vq;
-            if (ln < q) L.R[roff(q) + ln] = dj;
-            if (ln == q) { L.R[roff(q) + q] = rqq; rinv[q] = 1.0 / rqq; act = p; }
+            if (MPCQP_REG_RINV) {
+                // R^-1 of [[R, d1], [0, r_qq]]: column q = (-R^-1 d1 / r_qq, 1 / r_qq), and
+                // R^-1 d1 is this pass's r
+                const double irq = 1.0 / rqq;
+                if (ln < q) L.R[lrow(q) + ln] = -r * irq;
+                if (ln == q) { L.R[lrow(q) + q] = irq; act = p; }
+            } else {
+                if (ln < q) L.R[roff(q) + ln] = dj;
+                if (ln == q) { L.R[roff(q) + q] = rqq; rinv[q] = 1.0 / rqq; act = p; }
+            }
             if (ln == 0) L.st[p] = 2;
             ++q;
             fresh = true;
@@ -462,9 +500,63 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                 const int an = __shfl(act, src, kWave);
                 if (ln >= k && ln < q) { u = un; act = an; }
             }
+            if (MPCQP_REG_RINV) {
+                // R^-1 G' with the rotations that zero row k of R^-1 left of column q-1 (the G
+                // that restores R without column k), row k deleted, the last column dropped.
+                // Rotation j (lane j): hypotenuse sqrt(R^-1(k,k)^2 + sum_{i <= j} R^-1(k,i+1)^2)
+                // from one DPP prefix sum; c = R^-1(k,j+1) / h_j, s = -h_{j-1} / h_j.
+                const int qn = q - 1;
+                const double ra0 = L.R[lrow(k) + k];
+                const bool on = ln >= k && ln < qn;
+                const double rb = on ? L.R[lrow(ln + 1) + k] : 0.0;
+                double pf = wave_prefix_sum(rb * rb);
+                pin(pf);  // the DPP moves with every lane active (a disabled source lane reads 0)
+                const double H = sqrt(ra0 * ra0 + pf);
+                double hp = wave_prev(H);
+                pin(hp);
+                if (ln < NF) {
+                    const double ih = 1.0 / H;
+                    rot[2 * ln] = on ? rb * ih : 1.0;
+                    rot[2 * ln + 1] = on ? -(ln == k ? ra0 : hp) * ih : 0.0;
+                }
+                wave_sync();
+                // lane i carries row i: column j's rotated value is final (stored at row i, or
+                // i - 1 past the deleted row k); the carry is column j + 1 as rotated so far
+                double cr = (ln <= k) ? L.R[lrow(k) + ln] : 0.0;
+                int j = k;
+                for (; j + 4 <= qn; j += 4) {
+                    double c4[4], s4[4], y4[4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        c4[t] = rot[2 * (j + t)];
+                        s4[t] = rot[2 * (j + t) + 1];
+                        const double y = L.R[ln <= j + t + 1 ? lrow(j + t + 1) + ln : 0];
+                        y4[t] = (ln <= j + t + 1) ? y : 0.0;
+                    }
+                    step_fence();  // every load of the block before its stores (other lanes')
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const double o = c4[t] * cr + s4[t] * y4[t];
+                        cr = -s4[t] * cr + c4[t] * y4[t];
+                        if (ln <= j + t + 1 && ln != k) L.R[lrow(j + t) + ln - (ln > k ? 1 : 0)] = o;
+                    }
+                    step_fence();
+                }
+                for (; j < qn; ++j) {
+                    const double c = rot[2 * j], s_ = rot[2 * j + 1];
+                    const double y0 = L.R[ln <= j + 1 ? lrow(j + 1) + ln : 0];
+                    const double y = (ln <= j + 1) ? y0 : 0.0;
+                    step_fence();
+                    const double o = c * cr + s_ * y;
+                    cr = -s_ * cr + c * y;
+                    if (ln <= j + 1 && ln != k) L.R[lrow(j) + ln - (ln > k ? 1 : 0)] = o;
+                    step_fence();
+                }
+                --q;
+            }
             // R's columns k+1.. move one left: lane l moves its own entries (rows <= j + 1 of
             //      column j + 1), so no lane waits on another -- four columns per round trip
-            for (int j = k; j < q - 1; j += 4) {
+            for (int j = k; !MPCQP_REG_RINV && j < q - 1; j += 4) {
                 double v[4];
 #pragma unroll
                 for (int t = 0; t < 4; ++t)
@@ -473,8 +565,10 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                 for (int t = 0; t < 4; ++t)
                     if (j + t < q - 1 && ln <= j + t + 1) L.R[roff(j + t) + ln] = v[t];
             }
-            --q;
-            if (ln < NF) { rot[2 * ln] = 1.0; rot[2 * ln + 1] = 0.0; }
+            if (!MPCQP_REG_RINV) {
+                --q;
+                if (ln < NF) { rot[2 * ln] = 1.0; rot[2 * ln + 1] = 0.0; }
+            }
             wave_sync();
             // Givens back to triangular.  Rotation j mixes rows j and j+1 of the columns
             // l > j (lane l - j - 1).  Row j+1 is untouched until then (prefetchable from LDS);
@@ -482,7 +576,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             // wave_shl), and the next pivot R(j+1, j+1) is lane 0's second output: the chain
             // from one rotation to the next stays in registers.  Same arithmetic as the
             // LDS round-trip form.
-            if (k < q) {
+            if (!MPCQP_REG_RINV && k < q) {
                 double carry = 0.0;  // row j of columns j+1+ln, after the previous rotation
                 {
                     const int l = k + 1 + ln;
