@@ -427,563 +427,569 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     MPCQP_STAMP(a.stamps, 1, tst);
     MPCQP_CUT(a.cut, 2);
 
-    // ---- g (lane p: g_p), then H_FF over the dead early view (lane p loads row p)
-    const bool ok = valid && status == ST_OK && nf > 0;
-    double gp = 0.0;
-    if (ok && hl < nf) {
-        const int vi = fid[hl], ki = vi / NU, ci = vi % NU;
-        double s = 0.0;
-#pragma unroll
-        for (int m = 1; m <= N; ++m) {  // m > ki; unrolled, branch-free: the loads issue together
-            const double beta = (double)(m - 1 - ki) + 0.5;
-            const double tm = UV[(m * 2 + 0) * NU + ci] + beta * UV[(m * 2 + 1) * NU + ci];
-            s += (m > ki) ? tm : 0.0;
-        }
-        gp = 2.0 * s;
-    }
-    wave_sync();
-    double *Hb = D + Lay::oR;
-    if (ok) {
-        // one lane per block pair (ki >= kj); the beta sums once per block
-        constexpr int NPAIR = N * (N + 1) / 2;
-        constexpr int NFT = NU / 3;
-        static_assert(NU % 3 == 0, "inputs are force triples");
-        for (int bp = hl; bp < NPAIR; bp += kHalf) {
-            // bp = ki (ki + 1) / 2 + kj, row-major over ki >= kj (closed form, corrected)
-            int ki = (int)((__builtin_sqrtf(8.0f * (float)bp + 1.0f) - 1.0f) * 0.5f);
-            ki += ((ki + 1) * (ki + 2) / 2 <= bp) ? 1 : 0;
-            ki -= (ki * (ki + 1) / 2 > bp) ? 1 : 0;
-            const int kj = bp - ki * (ki + 1) / 2;
-            double c, si, sj, sij;
-            beta_sums(ki + 1, N - 1, ki, kj, c, si, sj, sij);
-            const double bi = (double)(N - 1 - ki) + 0.5, bj = (double)(N - 1 - kj) + 0.5;
-            const double bij = bi * bj;
-            const double rf = (ki == kj) ? 1.0 : 0.0;  // R on the diagonal blocks (exact: fma by 1)
-            // the free inputs of a step come in whole force triples (a foot in contact has
-            // all three components free: the fast path's bounds guarantee it), so the block
-            // is a set of 3x3 foot-pair sub-blocks with consecutive positions.  The triples of
-            // each step are compacted (slot a: foot fI[a] at position pI[a], -1 past the step's
-            // count), so a sub-block slot no lane of the wave has is skipped as a whole: one
-            // stance foot per step (config B) runs one 3x3 sub-block per block pair, not four
-            int pI[NFT], pJ[NFT], fI[NFT], fJ[NFT];
-#pragma unroll
-            for (int t = 0; t < NFT; ++t) { pI[t] = pJ[t] = -1; fI[t] = fJ[t] = 0; }
-            int nI = 0, nJ = 0;
-#pragma unroll
-            for (int s_ = 0; s_ < NFT; ++s_) {
-                const int p_i = pos[ki * NU + 3 * s_], p_j = pos[kj * NU + 3 * s_];
-#pragma unroll
-                for (int t = 0; t < NFT; ++t) {
-                    const bool ti = p_i >= 0 && nI == t, tj = p_j >= 0 && nJ == t;
-                    pI[t] = ti ? p_i : pI[t];
-                    fI[t] = ti ? s_ : fI[t];
-                    pJ[t] = tj ? p_j : pJ[t];
-                    fJ[t] = tj ? s_ : fJ[t];
-                }
-                nI += p_i >= 0 ? 1 : 0;
-                nJ += p_j >= 0 ? 1 : 0;
+    // a wavefront with nothing to solve (both halves deferred, infeasible, nothing free, past
+    // the batch: B standing's every wavefront) goes straight to the outputs
+    double fval = 0.0, x = 0.0;
+    int iters = 0;
+    if (work) {
+        // ---- g (lane p: g_p), then H_FF over the dead early view (lane p loads row p)
+        const bool ok = valid && status == ST_OK && nf > 0;
+        double gp = 0.0;
+        if (ok && hl < nf) {
+            const int vi = fid[hl], ki = vi / NU, ci = vi % NU;
+            double s = 0.0;
+    #pragma unroll
+            for (int m = 1; m <= N; ++m) {  // m > ki; unrolled, branch-free: the loads issue together
+                const double beta = (double)(m - 1 - ki) + 0.5;
+                const double tm = UV[(m * 2 + 0) * NU + ci] + beta * UV[(m * 2 + 1) * NU + ci];
+                s += (m > ki) ? tm : 0.0;
             }
-#pragma unroll
-            for (int ta = 0; ta < NFT; ++ta) {
-#pragma unroll
-                for (int tb = 0; tb < NFT; ++tb) {
-                    if (pI[ta] < 0 || pJ[tb] < 0) continue;
-#pragma unroll
-                    for (int a3 = 0; a3 < 3; ++a3) {
-#pragma unroll
-                        for (int b3 = 0; b3 < 3; ++b3) {
-                            const int pp = pI[ta] + a3, qq = pJ[tb] + b3;
-                            const int ci = 3 * fI[ta] + a3, cj = 3 * fJ[tb] + b3;
-                            // branch-free: the strictly upper entries of a diagonal block go
-                            // to the dump slot
-                            const double *So = S + (cj * NU + ci) * 4;
-                            double v = c * So[0] + sij * So[1];
-                            v += So[2] + bij * So[3];
-                            v = fma(rf, Rm[cj * NU + ci], v);
-                            Hb[pp >= qq ? lrow(pp) + qq : Lay::oDump - Lay::oR] = 2.0 * v;
+            gp = 2.0 * s;
+        }
+        wave_sync();
+        double *Hb = D + Lay::oR;
+        if (ok) {
+            // one lane per block pair (ki >= kj); the beta sums once per block
+            constexpr int NPAIR = N * (N + 1) / 2;
+            constexpr int NFT = NU / 3;
+            static_assert(NU % 3 == 0, "inputs are force triples");
+            for (int bp = hl; bp < NPAIR; bp += kHalf) {
+                // bp = ki (ki + 1) / 2 + kj, row-major over ki >= kj (closed form, corrected)
+                int ki = (int)((__builtin_sqrtf(8.0f * (float)bp + 1.0f) - 1.0f) * 0.5f);
+                ki += ((ki + 1) * (ki + 2) / 2 <= bp) ? 1 : 0;
+                ki -= (ki * (ki + 1) / 2 > bp) ? 1 : 0;
+                const int kj = bp - ki * (ki + 1) / 2;
+                double c, si, sj, sij;
+                beta_sums(ki + 1, N - 1, ki, kj, c, si, sj, sij);
+                const double bi = (double)(N - 1 - ki) + 0.5, bj = (double)(N - 1 - kj) + 0.5;
+                const double bij = bi * bj;
+                const double rf = (ki == kj) ? 1.0 : 0.0;  // R on the diagonal blocks (exact: fma by 1)
+                // the free inputs of a step come in whole force triples (a foot in contact has
+                // all three components free: the fast path's bounds guarantee it), so the block
+                // is a set of 3x3 foot-pair sub-blocks with consecutive positions.  The triples of
+                // each step are compacted (slot a: foot fI[a] at position pI[a], -1 past the step's
+                // count), so a sub-block slot no lane of the wave has is skipped as a whole: one
+                // stance foot per step (config B) runs one 3x3 sub-block per block pair, not four
+                int pI[NFT], pJ[NFT], fI[NFT], fJ[NFT];
+    #pragma unroll
+                for (int t = 0; t < NFT; ++t) { pI[t] = pJ[t] = -1; fI[t] = fJ[t] = 0; }
+                int nI = 0, nJ = 0;
+    #pragma unroll
+                for (int s_ = 0; s_ < NFT; ++s_) {
+                    const int p_i = pos[ki * NU + 3 * s_], p_j = pos[kj * NU + 3 * s_];
+    #pragma unroll
+                    for (int t = 0; t < NFT; ++t) {
+                        const bool ti = p_i >= 0 && nI == t, tj = p_j >= 0 && nJ == t;
+                        pI[t] = ti ? p_i : pI[t];
+                        fI[t] = ti ? s_ : fI[t];
+                        pJ[t] = tj ? p_j : pJ[t];
+                        fJ[t] = tj ? s_ : fJ[t];
+                    }
+                    nI += p_i >= 0 ? 1 : 0;
+                    nJ += p_j >= 0 ? 1 : 0;
+                }
+    #pragma unroll
+                for (int ta = 0; ta < NFT; ++ta) {
+    #pragma unroll
+                    for (int tb = 0; tb < NFT; ++tb) {
+                        if (pI[ta] < 0 || pJ[tb] < 0) continue;
+    #pragma unroll
+                        for (int a3 = 0; a3 < 3; ++a3) {
+    #pragma unroll
+                            for (int b3 = 0; b3 < 3; ++b3) {
+                                const int pp = pI[ta] + a3, qq = pJ[tb] + b3;
+                                const int ci = 3 * fI[ta] + a3, cj = 3 * fJ[tb] + b3;
+                                // branch-free: the strictly upper entries of a diagonal block go
+                                // to the dump slot
+                                const double *So = S + (cj * NU + ci) * 4;
+                                double v = c * So[0] + sij * So[1];
+                                v += So[2] + bij * So[3];
+                                v = fma(rf, Rm[cj * NU + ci], v);
+                                Hb[pp >= qq ? lrow(pp) + qq : Lay::oDump - Lay::oR] = 2.0 * v;
+                            }
                         }
                     }
                 }
             }
         }
-    }
-    // rows without a free variable (past nf, or a half with nothing to solve) are identity
-    // rows of the padded H_FF: written into the packed buffer (rare: only such waves pay), so
-    // every lane then loads its row unmasked (entries right of the diagonal are never read)
-    const bool pad = !ok || hl >= nf;
-    if (__ballot(pad && hl < NF) != 0ull) {
-        if (pad && hl < NF)
-            for (int q = 0; q <= hl; ++q) Hb[lrow(hl) + q] = (q == hl) ? 1.0 : 0.0;
-    }
-    wave_sync();
-    double h[NF];
-#pragma unroll
-    for (int q = 0; q < NF; ++q) h[q] = Hb[lrow(hl) + q];
-    wave_sync();
-    MPCQP_STAMP(a.stamps, 3, tst);
-    MPCQP_CUT(a.cut, 3);
+        // rows without a free variable (past nf, or a half with nothing to solve) are identity
+        // rows of the padded H_FF: written into the packed buffer (rare: only such waves pay), so
+        // every lane then loads its row unmasked (entries right of the diagonal are never read)
+        const bool pad = !ok || hl >= nf;
+        if (__ballot(pad && hl < NF) != 0ull) {
+            if (pad && hl < NF)
+                for (int q = 0; q <= hl; ++q) Hb[lrow(hl) + q] = (q == hl) ? 1.0 : 0.0;
+        }
+        wave_sync();
+        double h[NF];
+    #pragma unroll
+        for (int q = 0; q < NF; ++q) h[q] = Hb[lrow(hl) + q];
+        wave_sync();
+        MPCQP_STAMP(a.stamps, 3, tst);
+        MPCQP_CUT(a.cut, 3);
 
-    // ---- solver (gi_run_reg with NF = 30 per half)
-    constexpr bool kRinv = MPCQP_PAIR_RINV;
-    double *Lc = D + Lay::oR, *R = D + Lay::oR, *Ri = D + Lay::oR;  // R (or R^-1) over dead L
-    double *rowbuf = D + Lay::oRow, *colb = rowbuf + NP, *rot = rowbuf + 2 * NP,
-           *rinv = rowbuf + 4 * NP;
-    double fval = 0.0, x = 0.0, u = 0.0;
-    int iters = 0, q = 0, act = -1;
-    double Jr[NF];
-    double gv = gp;
-    const bool any_ok = __ballot(ok) != 0ull;
-    bool ok2 = ok;
-    if (any_ok) {
-        // ---- Cholesky fused with the inverse sweep.  Right-looking, lane l owns row l of H_FF
-        //      (identity padding beyond nf).  Step k's column of L, broadcast from LDS for the
-        //      trailing update, is also the operand of step k of the forward substitution
-        //      that turns lane c's e_c into column c of L^-1 (= row c of J, in registers): one
-        //      LDS read feeds two independent FMA streams.  Lane 31 of each half starts from g
-        //      instead and ends with t = L^-1 g.  Same operations in the same order as a
-        //      separate Cholesky then inverse sweep.
-        if (hl < NF) colb[hl] = gv;
-        wave_sync();
-        // (branch-free: every lane reads colb -- a uniform address, two values per b128 -- and
-        //  selects, instead of a predicated read per element)
-        const bool gl = hl == kHalf - 1;
-#pragma unroll
-        for (int l = 0; l < NF; ++l) {
-            double cbl = colb[l];
-            pin(cbl);  // (keeps the load unconditional: LLVM would sink it into a branch)
-            Jr[l] = gl ? cbl : ((hl == l) ? 1.0 : 0.0);
-        }
-        double piv = hbcast<0>(h[0]);
-        bool bad = !(piv > 0.0);
-        double ik = rsqrt_nr(piv);
-        // CB columns per LDS round trip: columns k+1 .. k+CB-1 are finished in registers from
-        // the panel's DPP-broadcast entries L(k+c, k+c'), then the CB columns are written and
-        // the trailing update reads them together.  Per element the operations and their
-        // order are those of CB single-column steps (bitwise the same factor and J).
-        constexpr int CB = MPCQP_CHOL_CB;
-        static_assert(NF % CB == 0, "whole column panels");
-#pragma unroll
-        for (int k = 0; k < NF; k += CB) {
-            double lk[CB], ikc[CB];
-            double bc[CB][CB];  // bc[c][c2] = L(k + c, k + c2), broadcast once: the panel update
-                                // and the inverse sweep's column both use it
-            ikc[0] = ik;
-            lk[0] = h[k] * ik;
-            h[k] = lk[0];
-#pragma unroll
-            for (int c = 1; c < CB; ++c) {
-#pragma unroll
-                for (int c2 = 0; c2 < c; ++c2) {
-                    bc[c][c2] = hbcast(lk[c2], k + c);
-                    h[k + c] -= lk[c2] * bc[c][c2];  // panel column c2's update
-                }
-                const double pc = hbcast(h[k + c], k + c);
-                bad |= !(pc > 0.0);
-                ikc[c] = rsqrt_nr(pc);
-                lk[c] = h[k + c] * ikc[c];
-                h[k + c] = lk[c];
-            }
-            double pivn = 1.0, ikn = 1.0;
-            if (k + CB < NF) {
-                double hn = h[k + CB < NF ? k + CB : k];  // on lane k+CB
-#pragma unroll
-                for (int c = 0; c < CB - 1; ++c) hn -= lk[c] * lk[c];
-                pivn = hbcast(hn - lk[CB - 1] * lk[CB - 1], k + CB);
-                bad |= !(pivn > 0.0);
-                ikn = rsqrt_nr(pivn);
-            }
-#pragma unroll
-            for (int c = 0; c < CB; ++c)
-                if (hl >= k + c && hl < NF) Lc[ccol(k + c, NF) + hl - k - c] = lk[c];
-#pragma unroll
-            for (int c = 0; c < CB; ++c) {
-#pragma unroll
-                for (int c2 = 0; c2 < c; ++c2) Jr[k + c] -= bc[c][c2] * Jr[k + c2];
-                Jr[k + c] *= ikc[c];
-            }
+        // ---- solver (gi_run_reg with NF = 30 per half)
+        constexpr bool kRinv = MPCQP_PAIR_RINV;
+        double *Lc = D + Lay::oR, *R = D + Lay::oR, *Ri = D + Lay::oR;  // R (or R^-1) over dead L
+        double *rowbuf = D + Lay::oRow, *colb = rowbuf + NP, *rot = rowbuf + 2 * NP,
+               *rinv = rowbuf + 4 * NP;
+        double u = 0.0;
+        int q = 0, act = -1;
+        double Jr[NF];
+        double gv = gp;
+        const bool any_ok = __ballot(ok) != 0ull;
+        bool ok2 = ok;
+        if (any_ok) {
+            // ---- Cholesky fused with the inverse sweep.  Right-looking, lane l owns row l of H_FF
+            //      (identity padding beyond nf).  Step k's column of L, broadcast from LDS for the
+            //      trailing update, is also the operand of step k of the forward substitution
+            //      that turns lane c's e_c into column c of L^-1 (= row c of J, in registers): one
+            //      LDS read feeds two independent FMA streams.  Lane 31 of each half starts from g
+            //      instead and ends with t = L^-1 g.  Same operations in the same order as a
+            //      separate Cholesky then inverse sweep.
+            if (hl < NF) colb[hl] = gv;
             wave_sync();
-#pragma unroll
-            for (int j = 0; j < NF; ++j) {
-                if (j >= k + CB) {
-                    double cv[CB];
-#pragma unroll
-                    for (int c = 0; c < CB; ++c) cv[c] = Lc[ccol(k + c, NF) + j - k - c];
-#pragma unroll
-                    for (int c = 0; c < CB; ++c) h[j] -= lk[c] * cv[c];
-#pragma unroll
-                    for (int c = 0; c < CB; ++c) Jr[j] -= cv[c] * Jr[k + c];
-                }
-                if ((j % MPCQP_CHOL_PF) == MPCQP_CHOL_PF - 1 && j >= k + CB) step_fence();
+            // (branch-free: every lane reads colb -- a uniform address, two values per b128 -- and
+            //  selects, instead of a predicated read per element)
+            const bool gl = hl == kHalf - 1;
+    #pragma unroll
+            for (int l = 0; l < NF; ++l) {
+                double cbl = colb[l];
+                pin(cbl);  // (keeps the load unconditional: LLVM would sink it into a branch)
+                Jr[l] = gl ? cbl : ((hl == l) ? 1.0 : 0.0);
             }
-#pragma unroll
-            for (int j = 0; j < NF; ++j)
-                if (j >= k) { pin(h[j]); pin(Jr[j]); }
-            piv = pivn;
-            ik = ikn;
-            pin(piv);
-            pin(ik);
-            step_fence();
-        }
-        if (ok && bad) status = ST_NOT_PD;
-        ok2 = ok && status == ST_OK;
-        MPCQP_STAMP(a.stamps, 5, tst);
-        MPCQP_CUT(a.cut, 4);
-        MPCQP_CUT(a.cut, 5);
-        // ---- unconstrained minimum x = -J t, objective -|t|^2 / 2
-        wave_sync();
-        if (hl == kHalf - 1) {
-#pragma unroll
-            for (int j = 0; j < NF; ++j) colb[j] = Jr[j];
-        }
-        wave_sync();
-        gv = (hl < NF) ? colb[hl] : 0.0;
-        double s4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int j = 0; j < NF; ++j) {
-            s4[j & 3] += Jr[j] * colb[j];
-            if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
-        }
-        x = (ok2 && hl < nf) ? -((s4[0] + s4[1]) + (s4[2] + s4[3])) : 0.0;
-        fval = half_sum(hl < nf ? gv * gv : 0.0);
-        fval = ok2 ? -0.5 * fval : 0.0;
-    }
-    MPCQP_STAMP(a.stamps, 7, tst);
-    MPCQP_CUT(a.cut, 6);
-
-    // ---- dual active-set loop (Goldfarb-Idnani), flattened: one add or drop per pass, the
-    //      wave running while either half has work.  Lane l owns variable l's two bound
-    //      constraints (ids l and l + nf): their b and eligibility live in registers, so the
-    //      most-violated search is register arithmetic plus one half-wave argmin.
-    //      Add step: J2 <- J2 (I - beta v v'), the Householder reflection that maps d2 to
-    //      |d2| e_q (v_q by Parlett's cancellation-free form).  It leaves the same first
-    //      column J2 d2 / |d2| and R column as the Givens chain of gi_reg.hpp / the oracle;
-    //      the trailing columns of J2 are another orthonormal basis of the same subspace, which
-    //      every later GI quantity (z = J2 J2' n, d1 = J1' n, r) is invariant to.  62 FMAs on
-    //      the resident rows instead of 30 rotations and their suffix-scan set-up.
-    //      Drop step: Givens restores R to triangular, the rotations go to LDS for J.
-    const int mt = 2 * nf;
-    const int max_iter = a.max_iter > 0 ? a.max_iter : 10 * (mt + nf + 1);
-    // bit 0 / 1: lower / upper bound inactive (eligible); bit 2: the variable is a vertical
-    // force.  A free variable is a force in contact (or a literal-model input), so its bounds
-    // follow from bit 2 alone: b of x >= lo is lo, b of -x >= -hi is -hi
-    int stb = 0;
-    if (ok2 && hl < nf) {
-        double lo, hi;
-        pair_bound<NU, MODEL>(a, contact, fid[hl], lo, hi);
-        stb = (lo > -kInfty ? 1 : 0) | (hi < kInfty ? 2 : 0) |
-              ((MODEL == 0 && (fid[hl] % NU) % 3 == 2) ? 4 : 0);
-    }
-    auto blo_of = [&](int sb) { return MODEL == 1 ? a.u_min : ((sb & 4) ? a.fz_min : -a.fxy_max); };
-    auto bhi_of = [&](int sb) { return MODEL == 1 ? -a.u_max : ((sb & 4) ? -a.fz_max : -a.fxy_max); };
-    const double blo = blo_of(stb), bhi = bhi_of(stb);  // (bit 2 of stb never changes)
-    const double tlo = -kFeasTol * (1.0 + fabs(blo)), thi = -kFeasTol * (1.0 + fabs(bhi));
-    bool done = !ok2;
-    bool fresh = true;
-    int p = 0;
-    // the partial multiplier of the constraint being added (slot q), in every lane of the half
-    double uadd = 0.0;
-    // a zero double (the masked reads of the R^-1 product point here)
-    constexpr int oZ = Lay::oRow + 4 * NP;
-    if (kRinv && hl == 0) D[oZ] = 0.0;
-    MPCQP_SUB_INIT(tsub);
-#ifdef MPCQP_STAMPS
-    unsigned long long npass = 0;  // passes of this wavefront (diagnostic slot 2)
-#endif
-    while (__ballot(!done) != 0ull) {
-#ifdef MPCQP_STAMPS
-        ++npass;
-#endif
-        double dj = 0.0, sp = 0.0, z = 0.0, zn = 0.0, zq = 0.0, r = 0.0, t1 = INFINITY,
-               t2 = INFINITY, t = 0.0, sg = 1.0, beta = 0.0, dqv = 0.0;
-        int kslot = 0x7fffffff, a_ = 0;
-        bool lower = true;
-        // a pass either steps on the selected constraint p or (first pass) only selects
-        const bool go = !done && !fresh;
-        if (go) {
-            // ---- d = J' n_p = sg J(a, :)': lane a publishes its J row and the slack of p;
-            //      every lane reads its d_j, then lanes j < q zero their slot, leaving d2 (the
-            //      inactive part, for z and the reflection) in the buffer
-            lower = p < nf;
-            a_ = lower ? p : p - nf;
-            sg = lower ? 1.0 : -1.0;
-            if (hl == a_) {
-#pragma unroll
-                for (int c = 0; c < NF; ++c) {
-                    rowbuf[c] = Jr[c];
-                }
-                rowbuf[NP - 1] = lower ? x - blo : -x - bhi;
-            }
-            wave_sync();
-            dj = (hl < nf) ? sg * rowbuf[hl] : 0.0;
-            sp = rowbuf[NP - 1];
-            if constexpr (kRinv) {
-                // r = R^-1 d(0:q): lane i < q takes row i of R^-1 (column-major packed, (i, j)
-                // at lrow(j) + i: consecutive lanes, consecutive addresses) against the
-                // published d (uniform address per half); independent products, no chain
-                // (masked terms read the zero slot: an address select instead of value selects)
-                const int qmax = max(__builtin_amdgcn_readlane(q, 0), __builtin_amdgcn_readlane(q, kHalf));
-                double r2[2] = {0.0, 0.0};
-                for (int j = 0; j < qmax; ++j) {
-                    const double rij = D[hl <= j ? Lay::oR + lrow(j) + hl : oZ];
-                    const double dv = D[j < q ? Lay::oRow + j : oZ];
-                    r2[j & 1] = fma(rij, dv, r2[j & 1]);
-                }
-                r = (hl < q) ? sg * (r2[0] + r2[1]) : 0.0;
-            }
-            if (hl < q) rowbuf[hl] = 0.0;  // after every lane's read (LDS keeps program order)
-            wave_sync();
-            if (iters >= max_iter) { status = ST_ITER_LIMIT; done = true; }
-        }
-        MPCQP_SUB(tsub, 0);
-        MPCQP_CUT(a.cut, 20);
-        const bool stepping = go && !done;
-        if (stepping) {
-            ++iters;
-            // |d(0:q)|^2 and |d(q+1:nf)|^2 in one two-sum pass; zn = |d2|^2 = zq + d_q^2 and
-            // dd = |d|^2 = zn + the first part
-            double sq = hl < q ? dj * dj : 0.0;
-            zq = (hl > q && hl < nf) ? dj * dj : 0.0;
-            half_sum2(sq, zq);
-            dqv = q < nf ? sg * rowbuf[q] : 0.0;  // d_q: slot q is not zeroed (only j < q)
-            zn = fma(dqv, dqv, zq);
-            const double dd = zn + sq;
-            double z4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int j = 0; j < NF; ++j) {
-                z4[j & 3] += Jr[j] * rowbuf[j];
-                if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
-            }
-            z = sg * ((z4[0] + z4[1]) + (z4[2] + z4[3]));
-            pin(z);  // here, not sunk to its use after the R solve: the row would stay live
-            if (q > 0) {
-                if constexpr (!kRinv) {
-                    // r = R^-1 d(0:q): uniform loop to the larger q of the two halves
-                    const int qmax = max(__builtin_amdgcn_readlane(q, 0), __builtin_amdgcn_readlane(q, kHalf));
-                    double val = dj;
-                    for (int j = qmax - 1; j >= 0; --j) {
-                        const double rj = hread_rt(val, j) * rinv[j];
-                        if (j < q) {
-                            if (hl == j) r = rj;
-                            if (hl < j) val -= R[roff(j) + hl] * rj;
-                        }
+            double piv = hbcast<0>(h[0]);
+            bool bad = !(piv > 0.0);
+            double ik = rsqrt_nr(piv);
+            // CB columns per LDS round trip: columns k+1 .. k+CB-1 are finished in registers from
+            // the panel's DPP-broadcast entries L(k+c, k+c'), then the CB columns are written and
+            // the trailing update reads them together.  Per element the operations and their
+            // order are those of CB single-column steps (bitwise the same factor and J).
+            constexpr int CB = MPCQP_CHOL_CB;
+            static_assert(NF % CB == 0, "whole column panels");
+    #pragma unroll
+            for (int k = 0; k < NF; k += CB) {
+                double lk[CB], ikc[CB];
+                double bc[CB][CB];  // bc[c][c2] = L(k + c, k + c2), broadcast once: the panel update
+                                    // and the inverse sweep's column both use it
+                ikc[0] = ik;
+                lk[0] = h[k] * ik;
+                h[k] = lk[0];
+    #pragma unroll
+                for (int c = 1; c < CB; ++c) {
+    #pragma unroll
+                    for (int c2 = 0; c2 < c; ++c2) {
+                        bc[c][c2] = hbcast(lk[c2], k + c);
+                        h[k + c] -= lk[c2] * bc[c][c2];  // panel column c2's update
                     }
+                    const double pc = hbcast(h[k + c], k + c);
+                    bad |= !(pc > 0.0);
+                    ikc[c] = rsqrt_nr(pc);
+                    lk[c] = h[k + c] * ikc[c];
+                    h[k + c] = lk[c];
                 }
-                const double rmax = half_max(hl < q ? fabs(r) : 0.0);
-                if (hl < q && r > kRTol * rmax) t1 = u / r;
-                kslot = half_argmin_lane(t1);
-            }
-            const bool dep = !(zn > kDepTol * dd);
-            t2 = dep ? INFINITY : -sp / zn;
-            t = t1 < t2 ? t1 : t2;
-            if (isinf(t)) { status = ST_INFEASIBLE; done = true; }
-        }
-        MPCQP_SUB(tsub, 1);
-        MPCQP_CUT(a.cut, 21);
-        const bool moving = stepping && !done;
-        bool add = false;
-        if (moving) {
-            const double uq = uadd;
-            if (!isinf(t2)) {
-                if (hl < nf) x += t * z;
-                fval += t * zn * (0.5 * t + uq);
-            }
-            if (hl < q) u -= t * r;
-            uadd += t;
-            if (hl == q) u = uadd;
-            add = !isinf(t2) && t2 <= t1;
-            if (add) {
-                // ---- add p: R column q = (d_0..d_{q-1}, r_qq); the reflection vector v = d2
-                //      - |d2| e_q goes to rowbuf (which holds d2 / sg), v = sg rowbuf
-                const double dq = dqv;
-                double rqq = dq, vq = 0.0;
-                if (zq > 0.0) {  // otherwise d2 = d_q e_q: no reflection, r_qq = d_q
-                    const double nrm = sqrt(zn);
-                    rqq = nrm;
-                    vq = dq > 0.0 ? -zq / (dq + nrm) : dq - nrm;
-                    beta = 2.0 / (vq * vq + zq);
+                double pivn = 1.0, ikn = 1.0;
+                if (k + CB < NF) {
+                    double hn = h[k + CB < NF ? k + CB : k];  // on lane k+CB
+    #pragma unroll
+                    for (int c = 0; c < CB - 1; ++c) hn -= lk[c] * lk[c];
+                    pivn = hbcast(hn - lk[CB - 1] * lk[CB - 1], k + CB);
+                    bad |= !(pivn > 0.0);
+                    ikn = rsqrt_nr(pivn);
+                }
+    #pragma unroll
+                for (int c = 0; c < CB; ++c)
+                    if (hl >= k + c && hl < NF) Lc[ccol(k + c, NF) + hl - k - c] = lk[c];
+    #pragma unroll
+                for (int c = 0; c < CB; ++c) {
+    #pragma unroll
+                    for (int c2 = 0; c2 < c; ++c2) Jr[k + c] -= bc[c][c2] * Jr[k + c2];
+                    Jr[k + c] *= ikc[c];
                 }
                 wave_sync();
-                if (hl == q) rowbuf[q] = sg * vq;
-                if constexpr (kRinv) {
-                    // R^-1 of [[R, d1], [0, rqq]] = [[R^-1, -R^-1 d1 / rqq], [0, 1 / rqq]], and
-                    // R^-1 d1 is this pass's r
-                    const double irq = 1.0 / rqq;
-                    if (hl < q) Ri[lrow(q) + hl] = -r * irq;
-                    if (hl == q) { Ri[lrow(q) + q] = irq; act = p; }
-                } else {
-                    if (hl < q) R[roff(q) + hl] = dj;
-                    if (hl == q) { R[roff(q) + q] = rqq; rinv[q] = 1.0 / rqq; act = p; }
-                }
-                if (hl == a_) stb &= lower ? ~1 : ~2;
-                ++q;
-                fresh = true;
-            } else {
-                // ---- drop slot kslot: shift u / act and R's columns left, then Givens back
-                //      to triangular; the (c, s) pairs go to LDS for J
-                const int k = kslot;
-                const int dropped = hread_k(act, k);
-                const bool dlow = dropped < nf;
-                if (hl == (dlow ? dropped : dropped - nf)) stb |= dlow ? 1 : 2;
-                {
-                    const int src = (hl + 1 < kHalf) ? ln + 1 : ln;
-                    const double un = __shfl(u, src, kWave);
-                    const int an = __shfl(act, src, kWave);
-                    if (hl >= k && hl < q) { u = un; act = an; }
-                }
-                if constexpr (kRinv) {
-                    // Removing column k of R and restoring the triangle with Givens G on rows
-                    // (j, j+1), j = k .. q-2, is, for R^-1, R^-1 G' with row k then deleted and the
-                    // last column dropped, where the same rotations zero row k of R^-1 G' left of
-                    // column q-1 (row k of (G R)^-1 is a multiple of e_{q-1}').  So the rotations
-                    // come from row k of R^-1 alone: every lane of the half runs the same chain
-                    // a <- hypot(a, R^-1(k, j+1)) on broadcast reads; (c, s) go to LDS for J.
-                    double ra = Ri[lrow(k) + k];
-                    rot[2 * hl] = 1.0;
-                    rot[2 * hl + 1] = 0.0;
-                    wave_sync();
-                    for (int j = k; j < q - 1; ++j) {
-                        const double rb = Ri[lrow(j + 1) + k];
-                        double c = 1.0, s_ = 0.0;
-                        if (ra != 0.0) {
-                            const double hh = sqrt(ra * ra + rb * rb), ih = 1.0 / hh;
-                            c = rb * ih;
-                            s_ = -ra * ih;
-                            ra = hh;
-                        } else {
-                            ra = rb;
-                        }
-                        // lane i's entries (i, j), (i, j+1) of R^-1 G' (rows i <= j+1 are
-                        // nonzero); rotated column j is final: it is written with row k deleted
-                        // (rows below k move up one, so it fits its j+1 packed slots again),
-                        // column j+1 goes back in place for the next rotation
-                        const double y0 = (hl <= j) ? Ri[lrow(j) + hl] : 0.0;
-                        const double y1 = (hl <= j + 1) ? Ri[lrow(j + 1) + hl] : 0.0;
-                        if (hl == 0) {
-                            rot[2 * j] = c;
-                            rot[2 * j + 1] = s_;
-                        }
-                        if (hl <= j + 1 && hl != k) Ri[lrow(j) + hl - (hl > k ? 1 : 0)] = c * y0 + s_ * y1;
-                        if (hl <= j + 1) Ri[lrow(j + 1) + hl] = -s_ * y0 + c * y1;
-                        wave_sync();
+    #pragma unroll
+                for (int j = 0; j < NF; ++j) {
+                    if (j >= k + CB) {
+                        double cv[CB];
+    #pragma unroll
+                        for (int c = 0; c < CB; ++c) cv[c] = Lc[ccol(k + c, NF) + j - k - c];
+    #pragma unroll
+                        for (int c = 0; c < CB; ++c) h[j] -= lk[c] * cv[c];
+    #pragma unroll
+                        for (int c = 0; c < CB; ++c) Jr[j] -= cv[c] * Jr[k + c];
                     }
-                    --q;
-                } else {
-                    for (int j = k; j < q - 1; ++j) {
-                        const double v = (hl <= j + 1) ? R[roff(j + 1) + hl] : 0.0;
-                        wave_sync();
-                        if (hl <= j + 1) R[roff(j) + hl] = v;
-                        wave_sync();
+                    if ((j % MPCQP_CHOL_PF) == MPCQP_CHOL_PF - 1 && j >= k + CB) step_fence();
+                }
+    #pragma unroll
+                for (int j = 0; j < NF; ++j)
+                    if (j >= k) { pin(h[j]); pin(Jr[j]); }
+                piv = pivn;
+                ik = ikn;
+                pin(piv);
+                pin(ik);
+                step_fence();
+            }
+            if (ok && bad) status = ST_NOT_PD;
+            ok2 = ok && status == ST_OK;
+            MPCQP_STAMP(a.stamps, 5, tst);
+            MPCQP_CUT(a.cut, 4);
+            MPCQP_CUT(a.cut, 5);
+            // ---- unconstrained minimum x = -J t, objective -|t|^2 / 2
+            wave_sync();
+            if (hl == kHalf - 1) {
+    #pragma unroll
+                for (int j = 0; j < NF; ++j) colb[j] = Jr[j];
+            }
+            wave_sync();
+            gv = (hl < NF) ? colb[hl] : 0.0;
+            double s4[4] = {0.0, 0.0, 0.0, 0.0};
+    #pragma unroll
+            for (int j = 0; j < NF; ++j) {
+                s4[j & 3] += Jr[j] * colb[j];
+                if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
+            }
+            x = (ok2 && hl < nf) ? -((s4[0] + s4[1]) + (s4[2] + s4[3])) : 0.0;
+            fval = half_sum(hl < nf ? gv * gv : 0.0);
+            fval = ok2 ? -0.5 * fval : 0.0;
+        }
+        MPCQP_STAMP(a.stamps, 7, tst);
+        MPCQP_CUT(a.cut, 6);
+
+        // ---- dual active-set loop (Goldfarb-Idnani), flattened: one add or drop per pass, the
+        //      wave running while either half has work.  Lane l owns variable l's two bound
+        //      constraints (ids l and l + nf): their b and eligibility live in registers, so the
+        //      most-violated search is register arithmetic plus one half-wave argmin.
+        //      Add step: J2 <- J2 (I - beta v v'), the Householder reflection that maps d2 to
+        //      |d2| e_q (v_q by Parlett's cancellation-free form).  It leaves the same first
+        //      column J2 d2 / |d2| and R column as the Givens chain of gi_reg.hpp / the oracle;
+        //      the trailing columns of J2 are another orthonormal basis of the same subspace, which
+        //      every later GI quantity (z = J2 J2' n, d1 = J1' n, r) is invariant to.  62 FMAs on
+        //      the resident rows instead of 30 rotations and their suffix-scan set-up.
+        //      Drop step: Givens restores R to triangular, the rotations go to LDS for J.
+        const int mt = 2 * nf;
+        const int max_iter = a.max_iter > 0 ? a.max_iter : 10 * (mt + nf + 1);
+        // bit 0 / 1: lower / upper bound inactive (eligible); bit 2: the variable is a vertical
+        // force.  A free variable is a force in contact (or a literal-model input), so its bounds
+        // follow from bit 2 alone: b of x >= lo is lo, b of -x >= -hi is -hi
+        int stb = 0;
+        if (ok2 && hl < nf) {
+            double lo, hi;
+            pair_bound<NU, MODEL>(a, contact, fid[hl], lo, hi);
+            stb = (lo > -kInfty ? 1 : 0) | (hi < kInfty ? 2 : 0) |
+                  ((MODEL == 0 && (fid[hl] % NU) % 3 == 2) ? 4 : 0);
+        }
+        auto blo_of = [&](int sb) { return MODEL == 1 ? a.u_min : ((sb & 4) ? a.fz_min : -a.fxy_max); };
+        auto bhi_of = [&](int sb) { return MODEL == 1 ? -a.u_max : ((sb & 4) ? -a.fz_max : -a.fxy_max); };
+        const double blo = blo_of(stb), bhi = bhi_of(stb);  // (bit 2 of stb never changes)
+        const double tlo = -kFeasTol * (1.0 + fabs(blo)), thi = -kFeasTol * (1.0 + fabs(bhi));
+        bool done = !ok2;
+        bool fresh = true;
+        int p = 0;
+        // the partial multiplier of the constraint being added (slot q), in every lane of the half
+        double uadd = 0.0;
+        // a zero double (the masked reads of the R^-1 product point here)
+        constexpr int oZ = Lay::oRow + 4 * NP;
+        if (kRinv && hl == 0) D[oZ] = 0.0;
+        MPCQP_SUB_INIT(tsub);
+    #ifdef MPCQP_STAMPS
+        unsigned long long npass = 0;  // passes of this wavefront (diagnostic slot 2)
+    #endif
+        while (__ballot(!done) != 0ull) {
+    #ifdef MPCQP_STAMPS
+            ++npass;
+    #endif
+            double dj = 0.0, sp = 0.0, z = 0.0, zn = 0.0, zq = 0.0, r = 0.0, t1 = INFINITY,
+                   t2 = INFINITY, t = 0.0, sg = 1.0, beta = 0.0, dqv = 0.0;
+            int kslot = 0x7fffffff, a_ = 0;
+            bool lower = true;
+            // a pass either steps on the selected constraint p or (first pass) only selects
+            const bool go = !done && !fresh;
+            if (go) {
+                // ---- d = J' n_p = sg J(a, :)': lane a publishes its J row and the slack of p;
+                //      every lane reads its d_j, then lanes j < q zero their slot, leaving d2 (the
+                //      inactive part, for z and the reflection) in the buffer
+                lower = p < nf;
+                a_ = lower ? p : p - nf;
+                sg = lower ? 1.0 : -1.0;
+                if (hl == a_) {
+    #pragma unroll
+                    for (int c = 0; c < NF; ++c) {
+                        rowbuf[c] = Jr[c];
                     }
-                    --q;
-                    rot[2 * hl] = 1.0;
-                    rot[2 * hl + 1] = 0.0;
-                    wave_sync();
-                    for (int j = k; j < q; ++j) {
-                        const double aa = R[roff(j) + j], bb = R[roff(j) + j + 1];
-                        if (bb != 0.0) {
-                            const double hh = sqrt(aa * aa + bb * bb);
-                            const double ih = 1.0 / hh;
-                            const double c = aa * ih, s_ = bb * ih;
-                            const int l = j + 1 + hl;
-                            double r0 = 0.0, r1 = 0.0;
-                            if (l < q) { r0 = R[roff(l) + j]; r1 = R[roff(l) + j + 1]; }
-                            wave_sync();
-                            if (l < q) {
-                                R[roff(l) + j] = c * r0 + s_ * r1;
-                                R[roff(l) + j + 1] = -s_ * r0 + c * r1;
+                    rowbuf[NP - 1] = lower ? x - blo : -x - bhi;
+                }
+                wave_sync();
+                dj = (hl < nf) ? sg * rowbuf[hl] : 0.0;
+                sp = rowbuf[NP - 1];
+                if constexpr (kRinv) {
+                    // r = R^-1 d(0:q): lane i < q takes row i of R^-1 (column-major packed, (i, j)
+                    // at lrow(j) + i: consecutive lanes, consecutive addresses) against the
+                    // published d (uniform address per half); independent products, no chain
+                    // (masked terms read the zero slot: an address select instead of value selects)
+                    const int qmax = max(__builtin_amdgcn_readlane(q, 0), __builtin_amdgcn_readlane(q, kHalf));
+                    double r2[2] = {0.0, 0.0};
+                    for (int j = 0; j < qmax; ++j) {
+                        const double rij = D[hl <= j ? Lay::oR + lrow(j) + hl : oZ];
+                        const double dv = D[j < q ? Lay::oRow + j : oZ];
+                        r2[j & 1] = fma(rij, dv, r2[j & 1]);
+                    }
+                    r = (hl < q) ? sg * (r2[0] + r2[1]) : 0.0;
+                }
+                if (hl < q) rowbuf[hl] = 0.0;  // after every lane's read (LDS keeps program order)
+                wave_sync();
+                if (iters >= max_iter) { status = ST_ITER_LIMIT; done = true; }
+            }
+            MPCQP_SUB(tsub, 0);
+            MPCQP_CUT(a.cut, 20);
+            const bool stepping = go && !done;
+            if (stepping) {
+                ++iters;
+                // |d(0:q)|^2 and |d(q+1:nf)|^2 in one two-sum pass; zn = |d2|^2 = zq + d_q^2 and
+                // dd = |d|^2 = zn + the first part
+                double sq = hl < q ? dj * dj : 0.0;
+                zq = (hl > q && hl < nf) ? dj * dj : 0.0;
+                half_sum2(sq, zq);
+                dqv = q < nf ? sg * rowbuf[q] : 0.0;  // d_q: slot q is not zeroed (only j < q)
+                zn = fma(dqv, dqv, zq);
+                const double dd = zn + sq;
+                double z4[4] = {0.0, 0.0, 0.0, 0.0};
+    #pragma unroll
+                for (int j = 0; j < NF; ++j) {
+                    z4[j & 3] += Jr[j] * rowbuf[j];
+                    if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
+                }
+                z = sg * ((z4[0] + z4[1]) + (z4[2] + z4[3]));
+                pin(z);  // here, not sunk to its use after the R solve: the row would stay live
+                if (q > 0) {
+                    if constexpr (!kRinv) {
+                        // r = R^-1 d(0:q): uniform loop to the larger q of the two halves
+                        const int qmax = max(__builtin_amdgcn_readlane(q, 0), __builtin_amdgcn_readlane(q, kHalf));
+                        double val = dj;
+                        for (int j = qmax - 1; j >= 0; --j) {
+                            const double rj = hread_rt(val, j) * rinv[j];
+                            if (j < q) {
+                                if (hl == j) r = rj;
+                                if (hl < j) val -= R[roff(j) + hl] * rj;
                             }
+                        }
+                    }
+                    const double rmax = half_max(hl < q ? fabs(r) : 0.0);
+                    if (hl < q && r > kRTol * rmax) t1 = u / r;
+                    kslot = half_argmin_lane(t1);
+                }
+                const bool dep = !(zn > kDepTol * dd);
+                t2 = dep ? INFINITY : -sp / zn;
+                t = t1 < t2 ? t1 : t2;
+                if (isinf(t)) { status = ST_INFEASIBLE; done = true; }
+            }
+            MPCQP_SUB(tsub, 1);
+            MPCQP_CUT(a.cut, 21);
+            const bool moving = stepping && !done;
+            bool add = false;
+            if (moving) {
+                const double uq = uadd;
+                if (!isinf(t2)) {
+                    if (hl < nf) x += t * z;
+                    fval += t * zn * (0.5 * t + uq);
+                }
+                if (hl < q) u -= t * r;
+                uadd += t;
+                if (hl == q) u = uadd;
+                add = !isinf(t2) && t2 <= t1;
+                if (add) {
+                    // ---- add p: R column q = (d_0..d_{q-1}, r_qq); the reflection vector v = d2
+                    //      - |d2| e_q goes to rowbuf (which holds d2 / sg), v = sg rowbuf
+                    const double dq = dqv;
+                    double rqq = dq, vq = 0.0;
+                    if (zq > 0.0) {  // otherwise d2 = d_q e_q: no reflection, r_qq = d_q
+                        const double nrm = sqrt(zn);
+                        rqq = nrm;
+                        vq = dq > 0.0 ? -zq / (dq + nrm) : dq - nrm;
+                        beta = 2.0 / (vq * vq + zq);
+                    }
+                    wave_sync();
+                    if (hl == q) rowbuf[q] = sg * vq;
+                    if constexpr (kRinv) {
+                        // R^-1 of [[R, d1], [0, rqq]] = [[R^-1, -R^-1 d1 / rqq], [0, 1 / rqq]], and
+                        // R^-1 d1 is this pass's r
+                        const double irq = 1.0 / rqq;
+                        if (hl < q) Ri[lrow(q) + hl] = -r * irq;
+                        if (hl == q) { Ri[lrow(q) + q] = irq; act = p; }
+                    } else {
+                        if (hl < q) R[roff(q) + hl] = dj;
+                        if (hl == q) { R[roff(q) + q] = rqq; rinv[q] = 1.0 / rqq; act = p; }
+                    }
+                    if (hl == a_) stb &= lower ? ~1 : ~2;
+                    ++q;
+                    fresh = true;
+                } else {
+                    // ---- drop slot kslot: shift u / act and R's columns left, then Givens back
+                    //      to triangular; the (c, s) pairs go to LDS for J
+                    const int k = kslot;
+                    const int dropped = hread_k(act, k);
+                    const bool dlow = dropped < nf;
+                    if (hl == (dlow ? dropped : dropped - nf)) stb |= dlow ? 1 : 2;
+                    {
+                        const int src = (hl + 1 < kHalf) ? ln + 1 : ln;
+                        const double un = __shfl(u, src, kWave);
+                        const int an = __shfl(act, src, kWave);
+                        if (hl >= k && hl < q) { u = un; act = an; }
+                    }
+                    if constexpr (kRinv) {
+                        // Removing column k of R and restoring the triangle with Givens G on rows
+                        // (j, j+1), j = k .. q-2, is, for R^-1, R^-1 G' with row k then deleted and the
+                        // last column dropped, where the same rotations zero row k of R^-1 G' left of
+                        // column q-1 (row k of (G R)^-1 is a multiple of e_{q-1}').  So the rotations
+                        // come from row k of R^-1 alone: every lane of the half runs the same chain
+                        // a <- hypot(a, R^-1(k, j+1)) on broadcast reads; (c, s) go to LDS for J.
+                        double ra = Ri[lrow(k) + k];
+                        rot[2 * hl] = 1.0;
+                        rot[2 * hl + 1] = 0.0;
+                        wave_sync();
+                        for (int j = k; j < q - 1; ++j) {
+                            const double rb = Ri[lrow(j + 1) + k];
+                            double c = 1.0, s_ = 0.0;
+                            if (ra != 0.0) {
+                                const double hh = sqrt(ra * ra + rb * rb), ih = 1.0 / hh;
+                                c = rb * ih;
+                                s_ = -ra * ih;
+                                ra = hh;
+                            } else {
+                                ra = rb;
+                            }
+                            // lane i's entries (i, j), (i, j+1) of R^-1 G' (rows i <= j+1 are
+                            // nonzero); rotated column j is final: it is written with row k deleted
+                            // (rows below k move up one, so it fits its j+1 packed slots again),
+                            // column j+1 goes back in place for the next rotation
+                            const double y0 = (hl <= j) ? Ri[lrow(j) + hl] : 0.0;
+                            const double y1 = (hl <= j + 1) ? Ri[lrow(j + 1) + hl] : 0.0;
                             if (hl == 0) {
-                                R[roff(j) + j] = hh;
-                                R[roff(j) + j + 1] = 0.0;
-                                rinv[j] = ih;
                                 rot[2 * j] = c;
                                 rot[2 * j + 1] = s_;
                             }
+                            if (hl <= j + 1 && hl != k) Ri[lrow(j) + hl - (hl > k ? 1 : 0)] = c * y0 + s_ * y1;
+                            if (hl <= j + 1) Ri[lrow(j + 1) + hl] = -s_ * y0 + c * y1;
                             wave_sync();
-                        } else {
-                            if (hl == 0) rinv[j] = 1.0 / aa;
+                        }
+                        --q;
+                    } else {
+                        for (int j = k; j < q - 1; ++j) {
+                            const double v = (hl <= j + 1) ? R[roff(j + 1) + hl] : 0.0;
                             wave_sync();
+                            if (hl <= j + 1) R[roff(j) + hl] = v;
+                            wave_sync();
+                        }
+                        --q;
+                        rot[2 * hl] = 1.0;
+                        rot[2 * hl + 1] = 0.0;
+                        wave_sync();
+                        for (int j = k; j < q; ++j) {
+                            const double aa = R[roff(j) + j], bb = R[roff(j) + j + 1];
+                            if (bb != 0.0) {
+                                const double hh = sqrt(aa * aa + bb * bb);
+                                const double ih = 1.0 / hh;
+                                const double c = aa * ih, s_ = bb * ih;
+                                const int l = j + 1 + hl;
+                                double r0 = 0.0, r1 = 0.0;
+                                if (l < q) { r0 = R[roff(l) + j]; r1 = R[roff(l) + j + 1]; }
+                                wave_sync();
+                                if (l < q) {
+                                    R[roff(l) + j] = c * r0 + s_ * r1;
+                                    R[roff(l) + j + 1] = -s_ * r0 + c * r1;
+                                }
+                                if (hl == 0) {
+                                    R[roff(j) + j] = hh;
+                                    R[roff(j) + j + 1] = 0.0;
+                                    rinv[j] = ih;
+                                    rot[2 * j] = c;
+                                    rot[2 * j + 1] = s_;
+                                }
+                                wave_sync();
+                            } else {
+                                if (hl == 0) rinv[j] = 1.0 / aa;
+                                wave_sync();
+                            }
                         }
                     }
                 }
             }
-        }
-        wave_sync();
-        MPCQP_SUB(tsub, 2);
-        MPCQP_CUT(a.cut, 22);
-        if (!done && fresh) {
-            // ---- most violated inactive bound (lowest id on ties): before the first step and
-            //      right after every add, so a half's last add also ends its solve (no checking
-            //      pass of its own, no update of J that nothing reads)
-            double best = INFINITY;
-            bool upb = false;  // the lane's candidate is its upper bound (id hl + nf)
-            if (stb & 1) {
-                const double s_ = x - blo;
-                if (s_ < tlo) best = s_;
+            wave_sync();
+            MPCQP_SUB(tsub, 2);
+            MPCQP_CUT(a.cut, 22);
+            if (!done && fresh) {
+                // ---- most violated inactive bound (lowest id on ties): before the first step and
+                //      right after every add, so a half's last add also ends its solve (no checking
+                //      pass of its own, no update of J that nothing reads)
+                double best = INFINITY;
+                bool upb = false;  // the lane's candidate is its upper bound (id hl + nf)
+                if (stb & 1) {
+                    const double s_ = x - blo;
+                    if (s_ < tlo) best = s_;
+                }
+                if (stb & 2) {
+                    const double s_ = -x - bhi;
+                    if ((s_ < thi) & (s_ < best)) { best = s_; upb = true; }
+                }
+                // lowest id among the lanes at the minimum: a lower bound (id hl) before any upper
+                // bound (hl + nf), each by lowest lane
+                const double bm = half_min(best);
+                const uint32_t hit = half_ballot(best == bm), hitl = half_ballot(best == bm && !upb);
+                const int bid = bm == INFINITY ? 0x7fffffff
+                              : hitl ? (int)__builtin_ctz(hitl) : (int)__builtin_ctz(hit) + nf;
+                if (bid == 0x7fffffff) {
+                    done = true;  // optimal
+                } else {
+                    p = bid;
+                    if (hl == q) u = 0.0;
+                    uadd = 0.0;
+                    fresh = false;
+                }
             }
-            if (stb & 2) {
-                const double s_ = -x - bhi;
-                if ((s_ < thi) & (s_ < best)) { best = s_; upb = true; }
+            // ---- the pass's update of J, as ONE chain of wave-uniform steps (no divergent
+            //      definition of Jr, so the register allocator keeps a single copy of it):
+            //      add -> J2 (I - beta v v'), v = sg rowbuf (the signs cancel: J_j -= beta (J .
+            //      rowbuf) rowbuf_j, f = 0 in a half that does not add); drop -> rotations from LDS,
+            //      the identity in a half that does not drop
+            const bool hh = moving && add && beta != 0.0 && !done;
+            const bool rt = moving && !add;
+            if (__ballot(hh) != 0ull) {
+                double w4[4] = {0.0, 0.0, 0.0, 0.0};
+    #pragma unroll
+                for (int j = 0; j < NF; ++j) {
+                    w4[j & 3] += Jr[j] * rowbuf[j];
+                    if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
+                }
+                const double f = hh ? beta * ((w4[0] + w4[1]) + (w4[2] + w4[3])) : 0.0;
+    #pragma unroll
+                for (int j = 0; j < NF; ++j) {
+                    Jr[j] -= f * rowbuf[j];
+                    if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
+                }
             }
-            // lowest id among the lanes at the minimum: a lower bound (id hl) before any upper
-            // bound (hl + nf), each by lowest lane
-            const double bm = half_min(best);
-            const uint32_t hit = half_ballot(best == bm), hitl = half_ballot(best == bm && !upb);
-            const int bid = bm == INFINITY ? 0x7fffffff
-                          : hitl ? (int)__builtin_ctz(hitl) : (int)__builtin_ctz(hit) + nf;
-            if (bid == 0x7fffffff) {
-                done = true;  // optimal
-            } else {
-                p = bid;
-                if (hl == q) u = 0.0;
-                uadd = 0.0;
-                fresh = false;
-            }
-        }
-        // ---- the pass's update of J, as ONE chain of wave-uniform steps (no divergent
-        //      definition of Jr, so the register allocator keeps a single copy of it):
-        //      add -> J2 (I - beta v v'), v = sg rowbuf (the signs cancel: J_j -= beta (J .
-        //      rowbuf) rowbuf_j, f = 0 in a half that does not add); drop -> rotations from LDS,
-        //      the identity in a half that does not drop
-        const bool hh = moving && add && beta != 0.0 && !done;
-        const bool rt = moving && !add;
-        if (__ballot(hh) != 0ull) {
-            double w4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int j = 0; j < NF; ++j) {
-                w4[j & 3] += Jr[j] * rowbuf[j];
-                if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
-            }
-            const double f = hh ? beta * ((w4[0] + w4[1]) + (w4[2] + w4[3])) : 0.0;
-#pragma unroll
-            for (int j = 0; j < NF; ++j) {
-                Jr[j] -= f * rowbuf[j];
-                if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
-            }
-        }
-        if (__ballot(rt) != 0ull) {
-            if (!rt) {
-                rot[2 * hl] = 1.0;
-                rot[2 * hl + 1] = 0.0;
+            if (__ballot(rt) != 0ull) {
+                if (!rt) {
+                    rot[2 * hl] = 1.0;
+                    rot[2 * hl + 1] = 0.0;
+                }
+                wave_sync();
+    #pragma unroll
+                for (int j = 0; j < NF - 1; ++j) {
+                    const double c = rot[2 * j], s_ = rot[2 * j + 1];
+                    const double y0 = Jr[j], y1 = Jr[j + 1];
+                    Jr[j] = c * y0 + s_ * y1;
+                    Jr[j + 1] = -s_ * y0 + c * y1;
+                    if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
+                }
             }
             wave_sync();
-#pragma unroll
-            for (int j = 0; j < NF - 1; ++j) {
-                const double c = rot[2 * j], s_ = rot[2 * j + 1];
-                const double y0 = Jr[j], y1 = Jr[j + 1];
-                Jr[j] = c * y0 + s_ * y1;
-                Jr[j + 1] = -s_ * y0 + c * y1;
-                if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
-            }
+            MPCQP_SUB(tsub, 3);
+            MPCQP_CUT(a.cut, 23);
         }
-        wave_sync();
-        MPCQP_SUB(tsub, 3);
-        MPCQP_CUT(a.cut, 23);
+        MPCQP_SUB_FLUSH(a.stamps, tsub);
+    #ifdef MPCQP_STAMPS
+        if (a.stamps && ln == 0) atomicAdd(&a.stamps[2], npass);
+    #endif
     }
-    MPCQP_SUB_FLUSH(a.stamps, tsub);
-#ifdef MPCQP_STAMPS
-    if (a.stamps && ln == 0) atomicAdd(&a.stamps[2], npass);
-#endif
 
     MPCQP_STAMP(a.stamps, 8, tst);
     MPCQP_CUT(a.cut, 7);
