@@ -105,9 +105,12 @@ constexpr int kSelWords = (kSelSlots + kSelTickets + 1) * kSelStride;
 // static __shared__ here would add to every kernel's LDS and cost the one-QP kernel a wave per CU.
 // groups: the workgroups 0 .. groups-1 that commit in a finalizing launch (the others must not
 // call; default the whole grid)
-__device__ __forceinline__ void sel_commit(const MpcArgs &a, unsigned long long k, int nV,
-                                           bool wrote, unsigned long long *scratch, int groups = -1) {
-    const int tid = (int)threadIdx.x, nt = (int)blockDim.x;
+// tid: the thread index (sel_commit passes threadIdx.x; a one-wave workgroup can pass its lane
+// id, so that threadIdx.x need not live in a register from the kernel's entry)
+__device__ __forceinline__ void sel_commit_t(const MpcArgs &a, unsigned long long k, int nV,
+                                             bool wrote, unsigned long long *scratch, int groups,
+                                             int tid) {
+    const int nt = (int)blockDim.x;
     int &sel_last = *reinterpret_cast<int *>(scratch + 16);
     unsigned long long *sel_red = scratch;
     unsigned long long *slot = &a.sel[(blockIdx.x % kSelSlots) * kSelStride];
@@ -168,6 +171,10 @@ __device__ __forceinline__ void sel_commit(const MpcArgs &a, unsigned long long 
     if (tid <= kSelTickets)
         __hip_atomic_store(tword(tid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid == 0) a.sel_rec[0] = (long long)m;
+}
+__device__ __forceinline__ void sel_commit(const MpcArgs &a, unsigned long long k, int nV,
+                                           bool wrote, unsigned long long *scratch, int groups = -1) {
+    sel_commit_t(a, k, nV, wrote, scratch, groups, (int)threadIdx.x);
 }
 
 // Overflow list (int words).  One counter per 128 B line would still take one device-scope
@@ -548,8 +555,8 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     double lin[8];
     mpc_load_inputs<Lay, NU, N, GEN>(a, b, D, lin);
     MPCQP_CUT(a.cut, 11);
-    mpc_model_terms<Lay, NU, MODEL>(a, D, lin);
-    MPCQP_CUT(a.cut, 13);
+    // the free map first (it reads only the bounds and the contact schedule): an instance the
+    // workgroup kernel takes returns before the model terms
     gi_setup(C);  // free map + constraint states
     if (C.nf > a.max_free) C.status = ST_BAD_DIMS;
     wave_sync();
@@ -557,6 +564,8 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
         if (ln == 0) wg_list_append(a.ovf, a.ovf_cap, b, true, 0, false);
         return;
     }
+    mpc_model_terms<Lay, NU, MODEL>(a, D, lin);
+    MPCQP_CUT(a.cut, 13);
     MPCQP_STAMP(a.stamps, 0, tst);
     MPCQP_CUT(a.cut, 1);
 

@@ -674,7 +674,9 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         int stb = 0;
         if (ok2 && hl < nf) {
             double lo, hi;
-            pair_bound<NU, MODEL>(a, contact, fid[hl], lo, hi);
+            // (a free variable is in contact: the all-ones schedule gives its bounds, and the
+            //  contact register need not live from the inputs to here)
+            pair_bound<NU, MODEL>(a, ~0ull, fid[hl], lo, hi);
             stb = (lo > -kInfty ? 1 : 0) | (hi < kInfty ? 2 : 0) |
                   ((MODEL == 0 && (fid[hl] % NU) % 3 == 2) ? 4 : 0);
         }
@@ -993,34 +995,42 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
 
     MPCQP_STAMP(a.stamps, 8, tst);
     MPCQP_CUT(a.cut, 7);
-    // ---- outputs
-    const int bo = (int)(long long)ctl[1];
+    // ---- outputs.  The lane-derived values (half lane, this half's LDS base and its free map)
+    // are re-derived here from an opaque lane id: kept from the start they were 3 of the
+    // kernel's spilled VGPRs
+    int lno = lane();
+    asm volatile("" : "+v"(lno));
+    const int hlo = lno & (kHalf - 1);
+    double *Do = reinterpret_cast<double *>(smem + (lno >= kHalf ? Lay::bytes : 0));
+    const int *fido = reinterpret_cast<const int *>(Do + Lay::nDoubles), *poso = fido + NF;
+    const uint64_t *ctlo = reinterpret_cast<const uint64_t *>(Do + Lay::oCt);
+    const int bo = (int)(long long)ctlo[1];
     const bool defer = a.ovf && nf > NF && nf <= a.max_free;  // the workgroup kernel takes it
     {  // one append (one atomic) for the wavefront's deferred instances
         const int b0 = __builtin_amdgcn_readlane(bo, 0), b1 = __builtin_amdgcn_readlane(bo, kHalf);
         const uint64_t dm = __ballot(defer && bo >= 0);
-        if (dm && ln == 0) wg_list_append(a.ovf, a.ovf_cap, b0, dm & 1ull, b1, (dm >> kHalf) & 1ull);
+        if (dm && lno == 0) wg_list_append(a.ovf, a.ovf_cap, b0, dm & 1ull, b1, (dm >> kHalf) & 1ull);
     }
     if (bo >= 0 && !defer) {
         // U assembled in LDS (the dead L / R space), then written once, coalesced: a
         // non-temporal store of a partial line is its own HBM write
-        const uint64_t cto = *ctl;
+        const uint64_t cto = *ctlo;
         double *U = a.U + (size_t)bo * NV;
-        double *Us = D + Lay::oR;
+        double *Us = Do + Lay::oR;
         const bool have_map = nf <= NF;
         wave_sync();
-        for (int v = hl; v < NV; v += kHalf) {
-            const int pv = pos[v];
+        for (int v = hlo; v < NV; v += kHalf) {
+            const int pv = poso[v];
             if (pv < 0 || !have_map) {
                 double lo, hi;
                 pair_bound<NU, MODEL>(a, cto, v, lo, hi);
                 Us[v] = (pv < 0) ? lo : 0.0;
             }
         }
-        if (have_map && hl < nf) Us[fid[hl]] = x;
+        if (have_map && hlo < nf) Us[fido[hlo]] = x;
         wave_sync();
-        for (int v = hl; v < NV; v += kHalf) stream_store(U + v, Us[v]);
-        if (hl == 0) {
+        for (int v = hlo; v < NV; v += kHalf) stream_store(U + v, Us[v]);
+        if (hlo == 0) {
             stream_store(a.cost + bo, fval);
             stream_store(a.status + bo, status);
             stream_store(a.iters + bo, iters);
@@ -1034,8 +1044,8 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             (bo >= 0 && !defer) ? sel_key(status, fval, a.sel_base + bo) : kSelNone;
         const unsigned long long k0 = readlane_u64(kh, 0), k1 = readlane_u64(kh, kHalf);
         wave_sync();  // the U staging reads are done: the L / R space is scratch again
-        sel_commit(a, k0 < k1 ? k0 : k1, NV, true,
-                   reinterpret_cast<unsigned long long *>(smem) + Lay::oR);
+        sel_commit_t(a, k0 < k1 ? k0 : k1, NV, true,
+                     reinterpret_cast<unsigned long long *>(smem) + Lay::oR, -1, lno);
     }
     MPCQP_STAMP(a.stamps, 9, tst);
     (void)NS;
