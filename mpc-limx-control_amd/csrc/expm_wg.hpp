@@ -164,6 +164,76 @@ __device__ __forceinline__ void wg_pade_solve(int nx, int ns, const double *U, c
     }
 }
 
+// The same Gauss-Jordan elimination (same pivots, lowest row on ties, same multipliers
+// l_i = D(i, k) / piv and updates) on ONE wavefront with the nx rows of every column in
+// registers (lane j = column j of [D | numer'], nx compile-time): the column-k entries reach all
+// lanes by v_readlane, the pivot row is chosen by lane k from its own registers and swapped by
+// selects -- no LDS and no barrier per column (the workgroup form above spent two barriers
+// and three LDS round trips per column: 426 k wave-cycles per QP at config E, a quarter of the
+// kernel).  MPCQP_PADE_WAVE=0 keeps the workgroup form (A/B builds).
+#ifndef MPCQP_PADE_WAVE
+#define MPCQP_PADE_WAVE 1
+#endif
+template <int NXC>
+__device__ __forceinline__ void wave_pade_gj(int ns, const double *U, const double *V, double *E) {
+    constexpr int nx = NXC;
+    const int j = lane(), ncol = nx + ns;
+    const bool colok = j < ncol;
+    double a[NXC];
+#pragma unroll
+    for (int i = 0; i < NXC; ++i) {
+        double v = 0.0;
+        if (colok) {
+            const int c = j < nx ? j : j - nx;
+            const int e = c * nx + i;
+            const double n = U[e] + V[e], d = -U[e] + V[e];
+            v = (j < nx) ? d : ((e / nx >= nx) ? n - d : n);
+        }
+        a[i] = v;
+    }
+#pragma unroll
+    for (int k = 0; k < NXC; ++k) {
+        // pivot: lane k's largest |a(i)|, i >= k (rows ascend: ties keep the lowest)
+        double best = -1.0;
+        int bi = k;
+#pragma unroll
+        for (int i = k; i < NXC; ++i) {
+            const double v = fabs(a[i]);
+            const bool t = v > best;
+            best = t ? v : best;
+            bi = t ? i : bi;
+        }
+        const int p = __builtin_amdgcn_readlane(bi, k);
+        double ck[NXC];  // column k before the swap, every lane
+#pragma unroll
+        for (int i = 0; i < NXC; ++i) ck[i] = readlane(a[i], k);
+        // rows k and p swap (p >= k, uniform)
+        double pk = a[k];
+#pragma unroll
+        for (int i = k + 1; i < NXC; ++i) pk = (p == i) ? a[i] : pk;
+        const double rk = a[k];
+#pragma unroll
+        for (int i = k + 1; i < NXC; ++i) a[i] = (p == i) ? rk : a[i];
+        a[k] = pk;
+        double ckk = ck[k];
+#pragma unroll
+        for (int i = k + 1; i < NXC; ++i) ckk = (p == i) ? ck[i] : ckk;  // = piv
+        const double rp = 1.0 / ckk;
+#pragma unroll
+        for (int i = 0; i < NXC; ++i) {
+            if (i == k) continue;
+            const double ci = (i > k && p == i) ? ck[k] : ck[i];  // row i's column-k entry after the swap
+            const bool upd = j > k && colok;
+            a[i] = upd ? a[i] - (ci * rp) * pk : a[i];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NXC; ++i) {
+        const double dii = readlane(a[i], i);
+        if (colok && j >= nx) E[(j - nx) * nx + i] = a[i] / dii;
+    }
+}
+
 // wave_expm by the workgroup (nt threads, nw waves).  T (nx x ns, scaled by Ts) is overwritten
 // when scaling; ws: 7 nx ns doubles; E: the result top block.  Every thread must call it.
 __device__ __forceinline__ void wg_expm(int nx, int ns, double *T, double *ws, double *E, int tid,
@@ -240,7 +310,9 @@ __device__ __forceinline__ void wg_expm(int nx, int ns, double *T, double *ws, d
         __syncthreads();
     }
     MPCQP_STAMP(stamps, 12, tx);
-    if (nx <= 6 * nw && nx + ns <= kWave && 4 * sz >= 352) {  // A2 .. W are dead here
+    if (MPCQP_PADE_WAVE && nx == 24 && nx + ns <= kWave) {  // config E
+        if (wv == 0) wave_pade_gj<24>(ns, U, V, E);
+    } else if (nx <= 6 * nw && nx + ns <= kWave && 4 * sz >= 352) {  // A2 .. W are dead here
         wg_pade_solve<6>(nx, ns, U, V, E, A2, wv, nw);         // config E: 24 rows, 4 waves
     } else if (nx <= 8 * nw && nx + ns <= kWave && 4 * sz >= 352) {
         wg_pade_solve<8>(nx, ns, U, V, E, A2, wv, nw);

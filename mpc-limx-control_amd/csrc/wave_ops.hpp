@@ -245,7 +245,12 @@ __device__ __forceinline__ void stream_store(T *p, T v) {
     } while (0)
 #define MPCQP_STAMP_INIT(t) unsigned long long t = __builtin_amdgcn_s_memtime()
 // sub-phases inside a loop: cycles accumulate in registers (no atomic per pass) and go to
-// slots 12..15 once, after the loop
+// slots 12..15 once, after the loop (MPCQP_SUB_OFF leaves 12..15 to the expm's sub-stamps)
+#ifdef MPCQP_SUB_OFF
+#define MPCQP_SUB_INIT(t) ((void)0)
+#define MPCQP_SUB(t, k) ((void)0)
+#define MPCQP_SUB_FLUSH(ptr, t) ((void)0)
+#else
 #define MPCQP_SUB_INIT(t) \
     unsigned long long t = __builtin_amdgcn_s_memtime(), t##_a0 = 0, t##_a1 = 0, t##_a2 = 0, t##_a3 = 0
 #define MPCQP_SUB(t, k)                                                         \
@@ -261,6 +266,7 @@ __device__ __forceinline__ void stream_store(T *p, T v) {
             atomicAdd(&(ptr)[14], t##_a2); atomicAdd(&(ptr)[15], t##_a3);      \
         }                                                                       \
     } while (0)
+#endif
 #else
 #define MPCQP_STAMP(ptr, k, t) ((void)0)
 #define MPCQP_STAMP_INIT(t) ((void)0)
