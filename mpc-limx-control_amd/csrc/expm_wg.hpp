@@ -176,6 +176,7 @@ __device__ __forceinline__ void wg_pade_solve(int nx, int ns, const double *U, c
 #endif
 template <int NXC>
 __device__ __forceinline__ void wave_pade_gj(int ns, const double *U, const double *V, double *E) {
+    static_assert(NXC <= 32, "pivot cases below");
     constexpr int nx = NXC;
     const int j = lane(), ncol = nx + ns;
     const bool colok = j < ncol;
@@ -193,31 +194,47 @@ __device__ __forceinline__ void wave_pade_gj(int ns, const double *U, const doub
     }
 #pragma unroll
     for (int k = 0; k < NXC; ++k) {
-        // pivot: lane k's largest |a(i)|, i >= k (rows ascend: ties keep the lowest)
-        double best = -1.0;
-        int bi = k;
+        // pivot: lane k's largest |a(i)|, i >= k, by a pairwise tree in which the lower row
+        // wins ties (the linear scan's rule: rows ascend, ties keep the lowest)
+        double tv[NXC];
+        int ti[NXC];
 #pragma unroll
-        for (int i = k; i < NXC; ++i) {
-            const double v = fabs(a[i]);
-            const bool t = v > best;
-            best = t ? v : best;
-            bi = t ? i : bi;
+        for (int i = k; i < NXC; ++i) { tv[i - k] = fabs(a[i]); ti[i - k] = i; }
+#pragma unroll
+        for (int w = 1; w < NXC - k; w *= 2) {
+#pragma unroll
+            for (int i = 0; i + w < NXC - k; i += 2 * w) {
+                const bool t = tv[i + w] > tv[i];
+                tv[i] = t ? tv[i + w] : tv[i];
+                ti[i] = t ? ti[i + w] : ti[i];
+            }
         }
-        const int p = __builtin_amdgcn_readlane(bi, k);
+        const int p = __builtin_amdgcn_readlane(ti[0], k);
         double ck[NXC];  // column k before the swap, every lane
 #pragma unroll
         for (int i = 0; i < NXC; ++i) ck[i] = readlane(a[i], k);
-        // rows k and p swap (p >= k, uniform)
-        double pk = a[k];
-#pragma unroll
-        for (int i = k + 1; i < NXC; ++i) pk = (p == i) ? a[i] : pk;
+        // rows k and p swap (p >= k, uniform: a scalar branch, no select chain)
+        double pk = a[k], ckk = ck[k];
         const double rk = a[k];
-#pragma unroll
-        for (int i = k + 1; i < NXC; ++i) a[i] = (p == i) ? rk : a[i];
-        a[k] = pk;
-        double ckk = ck[k];
-#pragma unroll
-        for (int i = k + 1; i < NXC; ++i) ckk = (p == i) ? ck[i] : ckk;  // = piv
+        switch (p) {
+#define MPCQP_PSW(i)                                          \
+    case i:                                                   \
+        if (i > k && i < NXC) {                               \
+            pk = a[i < NXC ? i : 0];                          \
+            ckk = ck[i < NXC ? i : 0];                        \
+            a[i < NXC ? i : 0] = rk;                          \
+        }                                                     \
+        break;
+            MPCQP_PSW(1) MPCQP_PSW(2) MPCQP_PSW(3) MPCQP_PSW(4) MPCQP_PSW(5) MPCQP_PSW(6)
+            MPCQP_PSW(7) MPCQP_PSW(8) MPCQP_PSW(9) MPCQP_PSW(10) MPCQP_PSW(11) MPCQP_PSW(12)
+            MPCQP_PSW(13) MPCQP_PSW(14) MPCQP_PSW(15) MPCQP_PSW(16) MPCQP_PSW(17) MPCQP_PSW(18)
+            MPCQP_PSW(19) MPCQP_PSW(20) MPCQP_PSW(21) MPCQP_PSW(22) MPCQP_PSW(23) MPCQP_PSW(24)
+            MPCQP_PSW(25) MPCQP_PSW(26) MPCQP_PSW(27) MPCQP_PSW(28) MPCQP_PSW(29) MPCQP_PSW(30)
+            MPCQP_PSW(31)
+#undef MPCQP_PSW
+            default: break;
+        }
+        a[k] = pk;  // ckk = piv
         const double rp = 1.0 / ckk;
 #pragma unroll
         for (int i = 0; i < NXC; ++i) {
