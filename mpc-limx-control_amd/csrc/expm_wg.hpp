@@ -55,6 +55,56 @@ __device__ __forceinline__ void wg_alg_mul(int nx, int ns, const double *X, cons
     __syncthreads();
 }
 
+// Two products in one pass (8 tiles over the waves, one barrier), each with its right operand a
+// linear combination and a combination added to its result (degree 13's W and V, which depend
+// only on A2, A4, A6):  out_p = X (sum_q cb_p[q] Mb_p[q]) + (sum_q ce_p[q] Me_p[q] + ceI_p I),
+// the right operands' scalar parts 0.  Every sum in alg_comb's order, so the values are those
+// of the comb / mul / add stages it replaces (five barriers fewer).
+template <int K>
+struct AlgComb {
+    double c[K];
+    const double *M[K];
+    __device__ __forceinline__ double at(int e) const {
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) s += c[q] * M[q][e];
+        return s;
+    }
+};
+template <int KB, int KE>
+__device__ __forceinline__ void wg_alg_mul_comb2(int nx, int ns, const double *X,
+                                                 const AlgComb<KB> (&cb)[2], const AlgComb<KE> (&ce)[2],
+                                                 const double (&ceI)[2], double *const (&out)[2],
+                                                 int wv, int nw) {
+    const int tm_n = (nx + 15) >> 4, tn_n = (ns + 15) >> 4, ks = (nx + 3) >> 2, nt1 = tm_n * tn_n;
+    const int ln = lane(), li = ln & 15, lk = ln >> 4;
+    for (int t = wv; t < 2 * nt1; t += nw) {
+        const int pr = t < nt1 ? 0 : 1, tt = t < nt1 ? t : t - nt1;
+        const int tm = tt % tm_n, tn = tt / tm_n;
+        const int i = tm * 16 + li, j = tn * 16 + li;
+        dx4 acc = {0.0, 0.0, 0.0, 0.0};
+        for (int s = 0; s < ks; ++s) {
+            const int kk = 4 * s + lk;
+            const bool oka = i < nx && kk < nx, okb = j < ns && kk < nx;
+            const double a = X[oka ? kk * nx + i : 0];
+            double b = cb[pr].at(okb ? j * nx + kk : 0);
+            if (okb && kk == j) b += 0.0;  // (alg_comb's identity term, cI = 0)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(oka ? a : 0.0, okb ? b : 0.0, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = tm * 16 + lk + 4 * r, col = tn * 16 + li;
+            if (row < nx && col < ns) {
+                const int e = col * nx + row;
+                double w = ce[pr].at(e);
+                if (row == col) w += ceI[pr];
+                out[pr][e] = acc[r] + w;
+            }
+        }
+    }
+    __syncthreads();
+}
+
 // out = sum_q c[q] M[q] + cI I (alg_comb) over every thread
 template <int K>
 __device__ __forceinline__ void wg_alg_comb(int nx, int ns, double *out, const double (&c)[K],
@@ -174,8 +224,15 @@ __device__ __forceinline__ void wg_pade_solve(int nx, int ns, const double *U, c
 #ifndef MPCQP_PADE_WAVE
 #define MPCQP_PADE_WAVE 1
 #endif
+// MPCQP_PADE_LDS: column k reaches the lanes through LDS (lane k writes it, every lane reads it
+// back at uniform addresses: 2 NXC / 2 b128 instructions) instead of 2 NXC v_readlane.
+// Measured slower (E 6.39 vs 6.31 ms at 16,384, alternating A/B): off
+#ifndef MPCQP_PADE_LDS
+#define MPCQP_PADE_LDS 0
+#endif
 template <int NXC>
-__device__ __forceinline__ void wave_pade_gj(int ns, const double *U, const double *V, double *E) {
+__device__ __forceinline__ void wave_pade_gj(int ns, const double *U, const double *V, double *E,
+                                             double *scr) {
     static_assert(NXC <= 32, "pivot cases below");
     constexpr int nx = NXC;
     const int j = lane(), ncol = nx + ns;
@@ -211,8 +268,19 @@ __device__ __forceinline__ void wave_pade_gj(int ns, const double *U, const doub
         }
         const int p = __builtin_amdgcn_readlane(ti[0], k);
         double ck[NXC];  // column k before the swap, every lane
+        if (MPCQP_PADE_LDS) {
+            if (j == k) {
 #pragma unroll
-        for (int i = 0; i < NXC; ++i) ck[i] = readlane(a[i], k);
+                for (int i = 0; i < NXC; ++i) scr[i] = a[i];
+            }
+            wave_sync();
+#pragma unroll
+            for (int i = 0; i < NXC; ++i) ck[i] = scr[i];
+            wave_sync();  // (the next column's writes after these reads)
+        } else {
+#pragma unroll
+            for (int i = 0; i < NXC; ++i) ck[i] = readlane(a[i], k);
+        }
         // rows k and p swap (p >= k, uniform: a scalar branch, no select chain)
         double pk = a[k], ckk = ck[k];
         const double rk = a[k];
@@ -250,6 +318,13 @@ __device__ __forceinline__ void wave_pade_gj(int ns, const double *U, const doub
         if (colok && j >= nx) E[(j - nx) * nx + i] = a[i] / dii;
     }
 }
+
+// 1: degree 13's two independent products fused with their combinations (wg_alg_mul_comb2):
+// five barriers fewer, but the fused operands' three loads per element stretch the products'
+// chains; measured slower (E 6.37 vs 6.31 ms at 16,384, alternating A/B): off
+#ifndef MPCQP_EXPM_FUSE
+#define MPCQP_EXPM_FUSE 0
+#endif
 
 // wave_expm by the workgroup (nt threads, nw waves).  T (nx x ns, scaled by Ts) is overwritten
 // when scaling; ws: 7 nx ns doubles; E: the result top block.  Every thread must call it.
@@ -314,21 +389,34 @@ __device__ __forceinline__ void wg_expm(int nx, int ns, double *T, double *ws, d
         wg_alg_mul(nx, ns, T, T, 0.0, A2, wv, nw);
         wg_alg_mul(nx, ns, A2, A2, 0.0, A4, wv, nw);
         wg_alg_mul(nx, ns, A4, A2, 0.0, A6, wv, nw);
-        wg_alg_comb<3>(nx, ns, V, {b[13], b[11], b[9]}, {A6, A4, A2}, 0.0, tid, nt);
-        wg_alg_mul(nx, ns, A6, V, 0.0, W, wv, nw);
-        wg_alg_comb<3>(nx, ns, A8, {b[7], b[5], b[3]}, {A6, A4, A2}, b[1], tid, nt);
-        for (int e = tid; e < sz; e += nt) W[e] += A8[e];
-        __syncthreads();
-        wg_alg_mul(nx, ns, T, W, b[1], U, wv, nw);
-        wg_alg_comb<3>(nx, ns, W, {b[12], b[10], b[8]}, {A6, A4, A2}, 0.0, tid, nt);
-        wg_alg_mul(nx, ns, A6, W, 0.0, V, wv, nw);
-        wg_alg_comb<3>(nx, ns, A8, {b[6], b[4], b[2]}, {A6, A4, A2}, b[0], tid, nt);
-        for (int e = tid; e < sz; e += nt) V[e] += A8[e];
-        __syncthreads();
+        if (MPCQP_EXPM_FUSE) {
+            // W = A6 (b13 A6 + b11 A4 + b9 A2) + (b7 A6 + b5 A4 + b3 A2 + b1 I) and
+            // V = A6 (b12 A6 + b10 A4 + b8 A2) + (b6 A6 + b4 A4 + b2 A2 + b0 I) in one pass
+            const AlgComb<3> cb[2] = {{{b[13], b[11], b[9]}, {A6, A4, A2}},
+                                      {{b[12], b[10], b[8]}, {A6, A4, A2}}};
+            const AlgComb<3> ce[2] = {{{b[7], b[5], b[3]}, {A6, A4, A2}},
+                                      {{b[6], b[4], b[2]}, {A6, A4, A2}}};
+            const double ceI[2] = {b[1], b[0]};
+            double *const outs[2] = {W, V};
+            wg_alg_mul_comb2(nx, ns, A6, cb, ce, ceI, outs, wv, nw);
+            wg_alg_mul(nx, ns, T, W, b[1], U, wv, nw);
+        } else {
+            wg_alg_comb<3>(nx, ns, V, {b[13], b[11], b[9]}, {A6, A4, A2}, 0.0, tid, nt);
+            wg_alg_mul(nx, ns, A6, V, 0.0, W, wv, nw);
+            wg_alg_comb<3>(nx, ns, A8, {b[7], b[5], b[3]}, {A6, A4, A2}, b[1], tid, nt);
+            for (int e = tid; e < sz; e += nt) W[e] += A8[e];
+            __syncthreads();
+            wg_alg_mul(nx, ns, T, W, b[1], U, wv, nw);
+            wg_alg_comb<3>(nx, ns, W, {b[12], b[10], b[8]}, {A6, A4, A2}, 0.0, tid, nt);
+            wg_alg_mul(nx, ns, A6, W, 0.0, V, wv, nw);
+            wg_alg_comb<3>(nx, ns, A8, {b[6], b[4], b[2]}, {A6, A4, A2}, b[0], tid, nt);
+            for (int e = tid; e < sz; e += nt) V[e] += A8[e];
+            __syncthreads();
+        }
     }
     MPCQP_STAMP(stamps, 12, tx);
     if (MPCQP_PADE_WAVE && nx == 24 && nx + ns <= kWave) {  // config E
-        if (wv == 0) wave_pade_gj<24>(ns, U, V, E);
+        if (wv == 0) wave_pade_gj<24>(ns, U, V, E, A2);  // A2 .. W are dead here
     } else if (nx <= 6 * nw && nx + ns <= kWave && 4 * sz >= 352) {  // A2 .. W are dead here
         wg_pade_solve<6>(nx, ns, U, V, E, A2, wv, nw);         // config E: 24 rows, 4 waves
     } else if (nx <= 8 * nw && nx + ns <= kWave && 4 * sz >= 352) {
