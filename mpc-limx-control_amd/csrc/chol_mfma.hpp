@@ -48,6 +48,12 @@ __device__ __forceinline__ int tix(int i, int j) { return i * (i + 1) / 2 + j; }
 // Cholesky of the 16 x 16 block in `tile` (lower triangle of the stored S = H_kk', i.e. of H_kk
 // as it is symmetric) and W = L^-1, on lanes 0..15 of the calling wave: lane i owns row i of L,
 // then lane c column c of W.  Writes W's slices over the tile and W' slices to wt.
+// MPCQP_DIAG_FUSED: W's forward substitution runs inside the factorisation (right-looking:
+// step k's broadcast L(j, k) feeds both the trailing update of row j and w[j] -= L(j, k) w[k]),
+// instead of a second sweep of 120 more v_readlane pairs after it.  0 keeps the two sweeps.
+#ifndef MPCQP_DIAG_FUSED
+#define MPCQP_DIAG_FUSED 1
+#endif
 __device__ __forceinline__ void diag_block_inverse(double *tile, double *wt, bool &bad) {
     const int ln = lane();
     const bool on = ln < 16;
@@ -57,6 +63,9 @@ __device__ __forceinline__ void diag_block_inverse(double *tile, double *wt, boo
     for (int j = 0; j < 16; ++j)
         a[j] = (on && j <= li) ? tile[64 * (li >> 2) + 16 * (li & 3) + j] : 0.0;
     double iq[16];
+    double w[16];  // lane c: column c of W = L^-1 (fused form: e_c, reduced step by step)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = (li == j) ? 1.0 : 0.0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const double piv = readlane(a[k], k);
@@ -65,20 +74,23 @@ __device__ __forceinline__ void diag_block_inverse(double *tile, double *wt, boo
         iq[k] = isq;
         const double lk = a[k] * isq;  // L(ln, k); on lane k, L(k, k) = piv / sqrt(piv)
         a[k] = lk;
+        if (MPCQP_DIAG_FUSED) w[k] *= isq;
 #pragma unroll
         for (int j = k + 1; j < 16; ++j) {
             const double ljk = readlane(lk, j);
             if (li > k) a[j] -= lk * ljk;
+            if (MPCQP_DIAG_FUSED) w[j] -= ljk * w[k];
         }
     }
-    // W = L^-1, lane c: column c by forward substitution (L entries are wave-uniform)
-    double w[16];
+    if (!MPCQP_DIAG_FUSED) {
+        // W = L^-1, lane c: column c by forward substitution (L entries are wave-uniform)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        double s = (li == i) ? 1.0 : 0.0;
+        for (int i = 0; i < 16; ++i) {
+            double s = (li == i) ? 1.0 : 0.0;
 #pragma unroll
-        for (int m = 0; m < i; ++m) s -= readlane(a[m], i) * w[m];
-        w[i] = s * iq[i];
+            for (int m = 0; m < i; ++m) s -= readlane(a[m], i) * w[m];
+            w[i] = s * iq[i];
+        }
     }
     if (on) {
 #pragma unroll

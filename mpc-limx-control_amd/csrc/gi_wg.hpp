@@ -123,6 +123,10 @@ __device__ __forceinline__ void wg_pick(const double *red, int o, double &v, int
 // sum of R^-1(k, k+1 .. j+1)^2), then each lane carries its row through the columns with the
 // column loads issued four at a time; 0: one rotation after the other, an LDS round trip and a
 // sqrt / divide on the chain per column
+// 1: the selection's bound states and b in registers at NF > 64 (below)
+#ifndef MPCQP_WG_STREG
+#define MPCQP_WG_STREG 1
+#endif
 #ifndef MPCQP_WG_PDROP
 #define MPCQP_WG_PDROP 1
 #endif
@@ -222,6 +226,18 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
         const int v = L.fid[r], k = v / P.nu, c = v % P.nu, sft = c / 3;
         if (c % 3 == 2 && ((P.contact >> (2 * k + sft)) & 1ull)) fbase = 2 * nf + 4 * (k * P.nfeet + sft);
     }
+    // row r's two bound states and b in registers (half 0): an add sets them from the uniform
+    // p, a drop's row re-reads them after the pass's last barrier; no LDS reads per selection.
+    // Only for NF > 64 (at NF = 64 the four registers cost 8 more spilled VGPRs)
+    constexpr bool kStReg = TWO && MPCQP_WG_STREG;
+    int s0r = 0, s1r = 0;
+    double b0r = 0.0, b1r = 0.0;
+    if (kStReg && h == 0 && r < nf) {
+        s0r = L.st[r];
+        s1r = L.st[r + nf];
+        b0r = L.cb[r];
+        b1r = L.cb[r + nf];
+    }
     MPCQP_SUB_INIT(tsub);
     while (!done) {
         MPCQP_SUB(tsub, 3);
@@ -230,8 +246,8 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             double best = INFINITY;
             int bid = 0x7fffffff;
             if (h == 0 && r < nf) {
-                const unsigned char s0 = L.st[r], s1 = L.st[r + nf];
-                const double b0 = L.cb[r], b1 = L.cb[r + nf];
+                const int s0 = kStReg ? s0r : L.st[r], s1 = kStReg ? s1r : L.st[r + nf];
+                const double b0 = kStReg ? b0r : L.cb[r], b1 = kStReg ? b1r : L.cb[r + nf];
                 if (s0 == 1) {
                     const double sl_ = x - b0;
                     if (sl_ < -kFeasTol * (1.0 + fabs(b0))) { best = sl_; bid = r; }
@@ -514,6 +530,10 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             }
         }
         const bool add = !isinf(t2) && t2 <= t1;
+        if (kStReg && add) {  // (L.st[p] = 2 below, by wave 0)
+            s0r = (p == r) ? 2 : s0r;
+            s1r = (p == r + nf) ? 2 : s1r;
+        }
         double beta = 0.0;
         if (add) {
             // ---- add p: the Householder reflection of gi_reg.hpp, v = d2 - |d2| e_q
@@ -797,6 +817,10 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             if (h == 1) rot_half(NH);
         }
         __syncthreads();
+        if (kStReg && !add && h == 0 && r < nf) {  // a drop set L.st[dropped] = 1 (wave 0, before the barrier)
+            s0r = L.st[r];
+            s1r = L.st[r + nf];
+        }
     }
     MPCQP_SUB(tsub, 3);
     MPCQP_SUB_FLUSH(C.stamps, tsub);
