@@ -394,6 +394,9 @@ def main():
     ap.add_argument("--selection-dry-run", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--select", choices=("fused", "separate"), default="fused",
                     help="selection record from the solve kernels (fused) or k_select_min")
+    ap.add_argument("--serial-select", action="store_true",
+                    help="N > 1: wait for each step's all-gather before the next solve (default: "
+                         "the collective of step s overlaps the solve of step s + 1)")
     args = ap.parse_args()
     fused = args.select == "fused"
 
@@ -410,7 +413,7 @@ def main():
     import torch.distributed as dist
 
     import mpcqp
-    from mpcqp.dist import decode_record, host_record, host_reduce_records, select_global
+    from mpcqp.dist import PipelinedSelect, decode_record, host_record, host_reduce_records
 
     dry = args.selection_dry_run
     if dry:
@@ -433,39 +436,50 @@ def main():
     s0, ns = shard(S_total, world, rank)
     i0, B = s0 * CANDIDATES, ns * CANDIDATES
 
-    def run_line(batch_local, index_base, steps, warmup):
+    def run_line(batch_local, index_base, steps, warmup, serial=False):
         """time `steps` steps of solve + selection on this rank's shard; returns
-        (elapsed max over ranks, kernel ms, select ms, best record, status, iters, eng)"""
+        (elapsed max over ranks, kernel ms, select ms, best record, status, iters, eng).
+        N > 1: one all-gather of the ranks' records per step (mpcqp.dist.PipelinedSelect: step
+        s's collective in flight while step s + 1 solves, unless serial; all of them complete
+        inside the timed region)."""
         Bl = batch_local["x0"].shape[0] if not dry else batch_local["B"]
-        rec = torch.zeros(1 + nV, dtype=torch.int64, device=dev)
-        gathered = torch.zeros((world, 1 + nV), dtype=torch.int64, device=dev)
-        # one rank: the record k_select_min writes IS the selection (no copy launch per step)
-        best = torch.zeros(1 + nV, dtype=torch.int64, device=dev) if world > 1 else rec
+        recs = [torch.zeros(1 + nV, dtype=torch.int64, device=dev) for _ in range(2)]
+        gathered = [torch.zeros((world, 1 + nV), dtype=torch.int64, device=dev) for _ in range(2)]
+        # one rank: the record the solve writes IS the selection (no copy launch per step)
+        best = torch.zeros(1 + nV, dtype=torch.int64, device=dev) if world > 1 else recs[0]
+        reduce = host_reduce_records if dry else None
         if dry:
             cost, status, U = batch_local["cost"], batch_local["status"], batch_local["U"]
             eng = None
 
-            def step():
+            def solve_into(rec):
                 rec.copy_(torch.from_numpy(host_record(cost, status, U, index_base)))
-                if world > 1:
-                    select_global(dist, rec, gathered, best, host_reduce_records)
-                # world == 1: best is rec
         else:
             from mpcqp.engine import BatchEngine
             eng = BatchEngine(p, device=local)
             d = eng.upload(batch_local)
+            reduce = eng.reduce_records
 
-            def step():
+            def solve_into(rec):
                 if fused:
                     eng.solve_select(d, rec, index_base=index_base)
                 else:
                     eng.solve(d)
                     eng.select_record(d, rec, index_base=index_base)
-                if world > 1:
-                    select_global(dist, rec, gathered, best, eng.reduce_records)
-                # world == 1: best is rec
+        pipe = PipelinedSelect(dist, recs, gathered, best, reduce) if world > 1 else None
+
+        def step():
+            if pipe is None:  # world == 1: best is recs[0]
+                solve_into(recs[0])
+                return
+            solve_into(pipe.record())
+            pipe.submit()
+            if serial:
+                pipe.drain()
 
         def sync():
+            if pipe is not None:
+                pipe.drain()
             if not dry:
                 torch.cuda.synchronize()
 
@@ -475,29 +489,11 @@ def main():
         if world > 1:
             dist.barrier()
         sync()
-        evs = None
-        if not dry:
-            stream = torch.cuda.current_stream()
-            evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+        # the timed region is the steps alone: no event record between or around them (each
+        # record is a marker packet on the stream, ~4 us apiece at small shards)
         t0 = time.perf_counter()
         for s in range(steps):
-            if dry:
-                step()
-                continue
-            e = evs[s]
-            e[0].record(stream)
-            if fused:  # selection record built by the solve kernels' last workgroup
-                eng.solve_select(d, rec, index_base=index_base)
-            else:
-                eng.solve(d)
-            e[1].record(stream)
-            e[2].record(stream)
-            if not fused:
-                eng.select_record(d, rec, index_base=index_base)
-            e[3].record(stream)
-            if world > 1:
-                select_global(dist, rec, gathered, best, eng.reduce_records)
-            # world == 1: best is rec
+            step()
         sync()
         if world > 1:
             dist.barrier()
@@ -510,6 +506,24 @@ def main():
         mpc_ms = sel_ms = None
         kern = {}
         if not dry:
+            # solve and selection durations: torch events around the calls, a separate pass of
+            # `steps` more steps after the timed ones
+            stream = torch.cuda.current_stream()
+            evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+            rec = recs[0]
+            for s in range(steps):
+                e = evs[s]
+                e[0].record(stream)
+                if fused:  # selection record built by the solve kernels' last workgroup
+                    eng.solve_select(d, rec, index_base=index_base)
+                else:
+                    eng.solve(d)
+                e[1].record(stream)
+                e[2].record(stream)
+                if not fused:
+                    eng.select_record(d, rec, index_base=index_base)
+                e[3].record(stream)
+            sync()
             mpc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
             sel_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
             if not args.no_kernel_timing:
@@ -541,8 +555,16 @@ def main():
         local_batch = slice_batch(full, i0, B)
         del full
     elapsed, mpc_ms, sel_ms, best, status, iters, eng, kern = run_line(
-        local_batch, i0, args.steps, args.warmup)
+        local_batch, i0, args.steps, args.warmup, serial=args.serial_select)
     bcost, bidx, bU = decode_record(best)
+    # N > 1: the same steps with each all-gather waited for before the next solve (reported
+    # beside the overlapped value, never as it)
+    serial_ms = None
+    if world > 1 and not args.serial_select:
+        el_s, *rest = run_line(local_batch, i0, args.steps, args.warmup, serial=True)
+        if rest[5] is not None:
+            rest[5].close()
+        serial_ms = el_s / args.steps * 1e3
 
     # ---- weak scaling (config D at N = 8): 65,536 per GPU, independent shards -------------
     weak = None
@@ -578,6 +600,12 @@ def main():
                               (" + one all-gather of [key | U] records + k_reduce_records"
                                if world > 1 else " (single GPU)")),
                    selected=dict(index=bidx, cost=bcost))
+        if world > 1:
+            cfg["selection_overlap"] = (
+                "serial: each all-gather waited for before the next solve" if args.serial_select
+                else "step s's all-gather in flight during step s + 1's solve (mpcqp.dist."
+                     "PipelinedSelect); every selection completes inside the timed region")
+            cfg["serial_select_ms_per_step"] = serial_ms
     if rank == 0 and dry:
         cfg["dry_run"] = "selection only: synthetic costs, gloo, no solve"
         out["config"] = cfg
@@ -592,7 +620,7 @@ def main():
         build = lib_build_id()
         kms = {k: v["ms"] for k, v in kern.items()}
         kms["mpcqp_batch_solve" + ("_select" if fused else "") +
-            " (timed steps, events around the call)"] = mpc_ms
+            " (events around the call, a pass after the timed steps)"] = mpc_ms
         if not fused:
             kms["k_select_min"] = sel_ms
         cfg.update(solved_frac=solved, mean_solver_iters=float(iters.mean()),

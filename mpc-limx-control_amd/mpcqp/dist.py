@@ -32,6 +32,50 @@ def select_global(dist, record, gathered, best, reduce):
     return best
 
 
+class PipelinedSelect:
+    """select_global over a stream of independent batches with the collective of batch s in
+    flight while batch s + 1 solves.
+
+    Two record / gather buffers alternate.  submit() starts batch s's all-gather asynchronously
+    (the backend orders it after the solve that wrote the record: RCCL waits on the current
+    stream) and then completes batch s - 1: work.wait() makes the current stream wait for that
+    collective, and the device reduction into `best` follows it.  So solve(s + 1), enqueued
+    after submit(s), waits only for the all-gather of s - 1, and the all-gather of s overlaps
+    it.  drain() completes the last batch.  Still one collective per batch; every batch's
+    selection is complete when drain() returns.  Buffer reuse is safe: record[i] is rewritten
+    by solve(s + 2), which the stream orders after wait(s); gathered[i] is refilled by the
+    all-gather of s + 2, which RCCL orders after the reduction of s on the current stream.
+    done: the number of batches whose selection has been reduced into `best`."""
+
+    def __init__(self, dist, records, gathered, best, reduce):
+        self.dist, self.records, self.gathered = dist, records, gathered
+        self.best, self.reduce = best, reduce
+        self.i = 0
+        self.pending = None
+        self.done = 0
+
+    def record(self):
+        """the record buffer the next batch's solve writes"""
+        return self.records[self.i]
+
+    def submit(self):
+        i = self.i
+        work = self.dist.all_gather_into_tensor(self.gathered[i].view(-1), self.records[i],
+                                                async_op=True)
+        self.drain()
+        self.pending = (work, i)
+        self.i ^= 1
+
+    def drain(self):
+        if self.pending is not None:
+            work, j = self.pending
+            work.wait()
+            self.reduce(self.gathered[j], self.best)
+            self.pending = None
+            self.done += 1
+        return self.best
+
+
 def decode_record(best) -> tuple:
     """(float32 cost or inf, global index or -1, U row float64) from a selection record"""
     b = np.asarray(best, dtype=np.int64)

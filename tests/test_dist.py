@@ -116,3 +116,66 @@ def test_host_record_roundtrip():
     np.testing.assert_array_equal(ub, np.concatenate(Us)[i0])
     none = host_record(np.zeros(3), np.ones(3, np.int32), np.ones((3, 7)))
     assert none[0] == NO_KEY and not none[1:].any()
+
+
+def _pipe_worker(rank, world, port, B, T, out_q):
+    sys.path.insert(0, os.path.join(ROOT, "mpc-limx-control_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    from mpcqp.dist import PipelinedSelect, decode_record, host_record, host_reduce_records
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    nV = 60
+    recs = [torch.zeros(1 + nV, dtype=torch.int64) for _ in range(2)]
+    gathered = [torch.zeros((world, 1 + nV), dtype=torch.int64) for _ in range(2)]
+    best = torch.zeros(1 + nV, dtype=torch.int64)
+    pipe = PipelinedSelect(dist, recs, gathered, best, host_reduce_records)
+    got = []
+    for t in range(T):  # batch t: costs seeded by (t, rank); every rank writes its own record
+        rng = np.random.default_rng(1000 * t + rank)
+        cost = rng.normal(size=B)
+        status = np.where(rng.random(B) < 0.2, 2, 0).astype(np.int32)
+        U = rng.normal(size=(B, nV))
+        pipe.record().copy_(torch.from_numpy(host_record(cost, status, U, rank * B)))
+        pipe.submit()  # completes batch t - 1
+        if t > 0:
+            got.append(decode_record(best.numpy())[:2])
+    pipe.drain()
+    got.append(decode_record(best.numpy())[:2])
+    out_q.put((rank, got, pipe.done))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_pipelined_selection_completes_every_batch():
+    """mpcqp.dist.PipelinedSelect (bench.py's N > 1 step: batch s's all-gather in flight while
+    batch s + 1 solves): after submit(s) the reduced record is batch s - 1's global argmin, and
+    drain() completes the last batch, on every rank."""
+    from mpcqp.dist import host_select
+
+    world, B, T = 2, 40, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_pipe_worker, args=(r, world, port, B, T, q)) for r in range(world)]
+    for pr in ps:
+        pr.start()
+    res = {}
+    for _ in range(world):
+        r, got, done = q.get(timeout=120)
+        res[r] = (got, done)
+    for pr in ps:
+        pr.join(timeout=60)
+    for t in range(T):
+        costs, status = [], []
+        for r in range(world):
+            rng = np.random.default_rng(1000 * t + r)
+            costs.append(rng.normal(size=B))
+            status.append(np.where(rng.random(B) < 0.2, 2, 0).astype(np.int32))
+        c, i = host_select(np.concatenate(costs), np.concatenate(status))
+        for r in range(world):
+            got, done = res[r]
+            assert done == T
+            assert got[t][1] == i and np.float32(got[t][0]) == np.float32(c), (t, r, got[t], c, i)

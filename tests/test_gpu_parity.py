@@ -744,23 +744,29 @@ def test_dense_full_size_properties(gpu, orc):
         assert u_close(U1[i], ref["U"][j]), i
 
 
-@pytest.mark.parametrize("config,gait,B", [("B", None, 4097), ("B", "standing", 512),
-                                           ("C", None, 384), ("C", "mixed", 384),
-                                           ("L", None, 300), ("E", None, 64)])
-def test_solve_select_fused_record(gpu, config, gait, B):
+@pytest.mark.parametrize("config,gait,B,max_free", [
+    ("B", None, 4097, None), ("B", "standing", 512, None), ("C", None, 384, None),
+    ("C", "mixed", 384, None), ("L", None, 300, None), ("E", None, 64, None),
+    ("B", None, 4097, 30), ("B", None, 33, 30), ("C", None, 384, 60)])
+def test_solve_select_fused_record(gpu, config, gait, B, max_free):
     """mpcqp_batch_solve_select: the record the fused kernels build (keys min-ed per workgroup,
     the batch's last workgroup copies the winner's U; the workgroup kernel finalizes when
     instances overflow to it) equals k_select_min's record of the same solve and the host
     restatement, bit for bit; repeated calls re-arm (same record), index_base offsets the key.
-    E runs the two-launch fallback."""
+    E runs the two-launch fallback.  max_free = 30 (a context that cannot overflow: no workgroup
+    kernel) makes the one-wave kernel's own last workgroup finalize."""
     import torch
     import mpcqp
     from mpcqp.dist import host_record
     from mpcqp.engine import BatchEngine
     p = mpcqp.model_params(config)
+    if max_free is not None:
+        p["max_free"] = max_free
     nV = p["nu"] * p["N"]
     batch = mpcqp.make_batch(p, B, seed=41, gait=gait) if gait else mpcqp.make_batch(p, B, seed=41)
     eng = BatchEngine(p)
+    if max_free is not None:
+        assert eng.fused_kernel in ("k_mpc_pair", "k_mpc")
     d = _prefilled(eng, batch)
     dev = torch.device("cuda:0")
     for base in (0, 123_457, 0):
