@@ -103,19 +103,49 @@ __device__ __forceinline__ void diag_block_inverse(double *tile, double *wt, boo
 
 // Blocked factorisation + inverse of the NF x NF matrix whose tiles are in F (TileFact layout),
 // by the workgroup's NW waves (wave index wv).  Returns the non-PD flag (same on every thread).
+// MPCQP_CHOL_LOOKAHEAD: the diagonal block k + 1 is updated first in step k's trailing update,
+// by wave 0, which then factors and inverts it at once while the other waves finish the step's
+// remaining tiles -- the serial 16-lane factorisation leaves the critical path of every step but
+// the first, and each step loses a barrier.  Same operations in the same order per element
+// (bit-identical).  0: the diagonal factorisation as its own stage (A/B builds).
+#ifndef MPCQP_CHOL_LOOKAHEAD
+#define MPCQP_CHOL_LOOKAHEAD 1
+#endif
 template <int NF, int NW>
 __device__ __forceinline__ bool chol_inverse_mfma(double *F, int wv) {
     using TF = TileFact<NF>;
     constexpr int T = TF::T, TS = TF::TS;
+    constexpr bool LA = MPCQP_CHOL_LOOKAHEAD && NW > 1;
     const int ln = lane();
     double *tiles = F + TF::oTiles, *Wt = F + TF::oWt;
     bool bad = false;
-    for (int k = 0; k < T; ++k) {
-        if (wv == 0) {
-            diag_block_inverse(tiles + TS * tix(k, k), Wt + TS * k, bad);
-            if (ln == 0 && bad) F[TF::oFlag] = 1.0;
-        }
+    auto diag = [&](int k) {
+        diag_block_inverse(tiles + TS * tix(k, k), Wt + TS * k, bad);
+        if (ln == 0 && bad) F[TF::oFlag] = 1.0;
+    };
+    // trailing pair t of step k (k < j <= i, row-major: t = 0 is the diagonal tile (k+1, k+1))
+    auto trail = [&](int k, int t) {
+        int i = k + 1, rem = t;
+        while (rem >= i - k) { rem -= i - k; ++i; }
+        const int j = k + 1 + rem;
+        const double *lj = tiles + TS * tix(j, k), *li = tiles + TS * tix(i, k);
+        double *c = tiles + TS * tix(i, j);
+        dx4 acc = {c[ln], c[64 + ln], c[128 + ln], c[192 + ln]};
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-lj[64 * s + ln], li[64 * s + ln], acc, 0, 0, 0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) c[64 * s + ln] = acc[s];
+    };
+    if (LA) {
+        if (wv == 0) diag(0);
         __syncthreads();
+    }
+    for (int k = 0; k < T; ++k) {
+        if (!LA) {
+            if (wv == 0) diag(k);
+            __syncthreads();
+        }
         // panel: L_ik' = W_k H_ik'
         for (int i = k + 1 + wv; i < T; i += NW) {
             const double *wk = Wt + TS * k;
@@ -127,24 +157,24 @@ __device__ __forceinline__ bool chol_inverse_mfma(double *F, int wv) {
 #pragma unroll
             for (int s = 0; s < 4; ++s) ti[64 * s + ln] = acc[s];
         }
+        if (k + 1 == T) break;  // (no trailing tile after the last panel: nothing follows)
         __syncthreads();
         // trailing update: H_ij' -= L_jk L_ik', k < j <= i (pairs in row-major order)
         const int np = (T - 1 - k) * (T - k) / 2;
-        for (int t = wv; t < np; t += NW) {
-            int i = k + 1, rem = t;
-            while (rem >= i - k) { rem -= i - k; ++i; }
-            const int j = k + 1 + rem;
-            const double *lj = tiles + TS * tix(j, k), *li = tiles + TS * tix(i, k);
-            double *c = tiles + TS * tix(i, j);
-            dx4 acc = {c[ln], c[64 + ln], c[128 + ln], c[192 + ln]};
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-lj[64 * s + ln], li[64 * s + ln], acc, 0, 0, 0);
-#pragma unroll
-            for (int s = 0; s < 4; ++s) c[64 * s + ln] = acc[s];
+        if (LA) {
+            if (wv == 0) {  // the next diagonal tile, then its factorisation (look-ahead)
+                trail(k, 0);
+                wave_sync();
+                diag(k + 1);
+            } else {
+                for (int t = wv; t < np; t += NW - 1) trail(k, t);
+            }
+        } else {
+            for (int t = wv; t < np; t += NW) trail(k, t);
         }
         __syncthreads();
     }
+    __syncthreads();
     // X = L^-1 below the diagonal, block row by block row
     constexpr int MAXJ = (T - 1 + NW - 1) / NW;
     for (int i = 1; i < T; ++i) {

@@ -210,15 +210,17 @@ __device__ __forceinline__ void dense_mpc_one(const MpcArgs &a, int b, unsigned 
     }
     __syncthreads();
     // ---- discretisation (the workgroup, matrix cores) and the free map / bounds (wave 0)
-    wg_expm(NX, NS, D + Lay::oT, D + Lay::oWs, AB, tid, NT, wv, NT / 64, a.stamps);
-    if (wv == 0) {
+    // (the free map and bounds touch only the solve-lifetime region and the int maps: the last
+    //  wave sets them up while the first solves the Pade quotient; C's fields are re-read from
+    //  oMisc / set uniformly below)
+    wg_expm(NX, NS, D + Lay::oT, D + Lay::oWs, AB, tid, NT, wv, NT / 64, a.stamps, [&]() {
         gi_setup(C);
         if (C.nf > a.max_free) C.status = ST_BAD_DIMS;
         if (ln == 0) {
             D[Lay::oMisc] = (double)C.nf;
             D[Lay::oMisc + 1] = (double)C.status;
         }
-    }
+    });
     __syncthreads();
     MPCQP_STAMP(a.stamps, 11, tst);
 

@@ -326,11 +326,18 @@ __device__ __forceinline__ void wave_pade_gj(int ns, const double *U, const doub
 #define MPCQP_EXPM_FUSE 0
 #endif
 
+struct NoSide {
+    __device__ void operator()() const {}
+};
 // wave_expm by the workgroup (nt threads, nw waves).  T (nx x ns, scaled by Ts) is overwritten
 // when scaling; ws: 7 nx ns doubles; E: the result top block.  Every thread must call it.
+// side: one wave's independent work (it must not touch T, ws or E), run by the last wave while
+// the first solves the Pade quotient alone (config E), else by the last wave after the solve.
+template <class Side = NoSide>
 __device__ __forceinline__ void wg_expm(int nx, int ns, double *T, double *ws, double *E, int tid,
                                         int nt, int wv, int nw,
-                                        unsigned long long *stamps = nullptr) {
+                                        unsigned long long *stamps = nullptr,
+                                        const Side &side = Side()) {
     MPCQP_STAMP_INIT(tx);
     const int sz = nx * ns;
     double *A2 = ws, *A4 = ws + sz, *A6 = ws + 2 * sz, *A8 = ws + 3 * sz, *U = ws + 4 * sz,
@@ -417,6 +424,7 @@ __device__ __forceinline__ void wg_expm(int nx, int ns, double *T, double *ws, d
     MPCQP_STAMP(stamps, 12, tx);
     if (MPCQP_PADE_WAVE && nx == 24 && nx + ns <= kWave) {  // config E
         if (wv == 0) wave_pade_gj<24>(ns, U, V, E, A2);  // A2 .. W are dead here
+        else if (wv == nw - 1) side();
     } else if (nx <= 6 * nw && nx + ns <= kWave && 4 * sz >= 352) {  // A2 .. W are dead here
         wg_pade_solve<6>(nx, ns, U, V, E, A2, wv, nw);         // config E: 24 rows, 4 waves
     } else if (nx <= 8 * nw && nx + ns <= kWave && 4 * sz >= 352) {
@@ -424,6 +432,7 @@ __device__ __forceinline__ void wg_expm(int nx, int ns, double *T, double *ws, d
     } else {
         if (wv == 0) expm_pade_solve(nx, ns, U, V, A2, E);
     }
+    if (!(MPCQP_PADE_WAVE && nx == 24 && nx + ns <= kWave) && wv == nw - 1) side();
     __syncthreads();
     MPCQP_STAMP(stamps, 13, tx);
     for (int s = 0; s < squarings; ++s) {

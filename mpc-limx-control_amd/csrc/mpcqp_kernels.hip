@@ -1458,11 +1458,13 @@ int mpcqp_batch_solve_select(mpcqp_ctx *c, int B, const double *x0, const double
     if (B < 0) return MPCQP_ERR_BAD_ARG;
     if (index_base < 0 || index_base + (int64_t)B > 0x7fffffffll) return MPCQP_ERR_BAD_DIMS;
     hipSetDevice(c->device);
-    if (B > 0 && c->fast && !c->fk.dense && (c->fk.wg || c->fk.pair || c->fk.mpc)) {
-        // the fused kernels min their keys into the context's selection words and the batch's
-        // last launch writes the record: the workgroup kernel (launched after the one-wave
-        // kernel on contexts that may overflow; its resident grid takes the tickets), else the
-        // one-wave kernel itself (max_free within its capacity): no selection launch
+    if (B > 0 && c->fast && !c->fk.dense && c->fk.wg) {
+        // the fused kernels min their keys into the context's selection words and the last
+        // workgroup of the workgroup kernel (always launched after the one-wave kernel on these
+        // contexts; its resident grid takes the tickets) writes the record: no selection launch.
+        // (Contexts without the workgroup kernel keep k_select_min: a ticket from every one-wave
+        // workgroup costs each an agent-scope release, an L2 write-back -- 1.10 ms per launch
+        // at 65,536 against 0.38 ms with the separate selection, r03s)
         if (!x0 || !xref || !lin || !U || !cost || !status || !iters) return MPCQP_ERR_BAD_ARG;
         if (c->m.model == MPCQP_MODEL_SRBM && !contact) return MPCQP_ERR_BAD_ARG;
         MpcArgs a = mpc_args(c, B);
