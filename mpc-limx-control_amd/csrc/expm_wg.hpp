@@ -230,6 +230,13 @@ __device__ __forceinline__ void wg_pade_solve(int nx, int ns, const double *U, c
 #ifndef MPCQP_PADE_LDS
 #define MPCQP_PADE_LDS 0
 #endif
+// MPCQP_PADE_NOSEL: every lane applies the step's update (no select keeping columns j <= k):
+// the columns left of k are never read again (their entries are garbage afterwards), and each
+// lane keeps its own pivot D(j, j) in a register from its step on.  The numerator columns
+// (j >= nx > k) get exactly the same operations, so E is bit-identical.
+#ifndef MPCQP_PADE_NOSEL
+#define MPCQP_PADE_NOSEL 1
+#endif
 template <int NXC>
 __device__ __forceinline__ void wave_pade_gj(int ns, const double *U, const double *V, double *E,
                                              double *scr) {
@@ -249,6 +256,7 @@ __device__ __forceinline__ void wave_pade_gj(int ns, const double *U, const doub
         }
         a[i] = v;
     }
+    double piv_own = 0.0;  // (MPCQP_PADE_NOSEL) lane j's pivot D(j, j), from step j on
 #pragma unroll
     for (int k = 0; k < NXC; ++k) {
         // pivot: lane k's largest |a(i)|, i >= k, by a pairwise tree in which the lower row
@@ -303,18 +311,23 @@ __device__ __forceinline__ void wave_pade_gj(int ns, const double *U, const doub
             default: break;
         }
         a[k] = pk;  // ckk = piv
+        if (MPCQP_PADE_NOSEL) piv_own = (j == k) ? pk : piv_own;
         const double rp = 1.0 / ckk;
 #pragma unroll
         for (int i = 0; i < NXC; ++i) {
             if (i == k) continue;
             const double ci = (i > k && p == i) ? ck[k] : ck[i];  // row i's column-k entry after the swap
-            const bool upd = j > k && colok;
-            a[i] = upd ? a[i] - (ci * rp) * pk : a[i];
+            if (MPCQP_PADE_NOSEL) {
+                a[i] = a[i] - (ci * rp) * pk;
+            } else {
+                const bool upd = j > k && colok;
+                a[i] = upd ? a[i] - (ci * rp) * pk : a[i];
+            }
         }
     }
 #pragma unroll
     for (int i = 0; i < NXC; ++i) {
-        const double dii = readlane(a[i], i);
+        const double dii = MPCQP_PADE_NOSEL ? readlane(piv_own, i) : readlane(a[i], i);
         if (colok && j >= nx) E[(j - nx) * nx + i] = a[i] / dii;
     }
 }
