@@ -54,6 +54,9 @@ __device__ __forceinline__ int tix(int i, int j) { return i * (i + 1) / 2 + j; }
 #ifndef MPCQP_DIAG_FUSED
 #define MPCQP_DIAG_FUSED 1
 #endif
+#ifndef MPCQP_DIAG_NOSEL
+#define MPCQP_DIAG_NOSEL 1
+#endif
 __device__ __forceinline__ void diag_block_inverse(double *tile, double *wt, bool &bad) {
     const int ln = lane();
     const bool on = ln < 16;
@@ -78,7 +81,10 @@ __device__ __forceinline__ void diag_block_inverse(double *tile, double *wt, boo
 #pragma unroll
         for (int j = k + 1; j < 16; ++j) {
             const double ljk = readlane(lk, j);
-            if (li > k) a[j] -= lk * ljk;
+            // (unmasked: a lane li <= k only changes its row's entries right of the diagonal,
+            //  which nothing reads -- lanes li < k hold zeros there and lk = 0 -- and no lane
+            //  reads another's row but through lk of lanes j > k)
+            if (MPCQP_DIAG_NOSEL || li > k) a[j] -= lk * ljk;
             if (MPCQP_DIAG_FUSED) w[j] -= ljk * w[k];
         }
     }
