@@ -3,7 +3,7 @@
 # never combined with trace domains).  Usage (GPU box, repo root): tools/pmc_stall.sh OUT
 set -o pipefail
 OUT=${1:-gpurun_out/stall}
-ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-per-config"
+ARGS=${ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline --no-per-config"}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 R=$(pwd)
