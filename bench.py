@@ -389,6 +389,9 @@ def main():
     ap.add_argument("--seed", type=int, default=20250404)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-per-config", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip the PCIe-inclusive, generated-input and per-tick lines (profiling "
+                         "runs: the host path launches the headline kernel too)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip the per-kernel timing pass after the timed steps")
     ap.add_argument("--selection-dry-run", action="store_true", help=argparse.SUPPRESS)
@@ -655,7 +658,7 @@ def main():
         out["roofline"] = roof
         if weak:
             cfg["weak"] = weak
-        if world == 1:
+        if world == 1 and not args.no_host_path:
             cfg["pcie_inclusive_qps"] = host_staged_rate(eng, local_batch, p)
             cfg["gait_fused_qps"] = gait_fused_rate(eng, p, B, args.seed)
             cfg["per_tick_latency"] = per_tick_latency(p, args.seed, device=local)

@@ -19,7 +19,10 @@ run() {  # name timeout cmd...
 }
 run bench 500 python3 bench.py
 grep '^{' $O/bench.log > $O/bench.json
-HB="--steps 20 --warmup 3 --no-cpu-baseline --no-per-config"
+# headline passes: a long warm-up so that the traced launches run at steady clocks (the first
+# ~60 launches of a fresh process ramp from ~400 to ~355 us), and no host-path lines (they
+# launch the same kernel and grid between PCIe copies)
+HB="--steps 20 --warmup ${HB_WARMUP:-100} --no-cpu-baseline --no-per-config --no-host-path"
 run B_trace 300 rocprofv3 --kernel-trace --stats -d $R/$O/B/trace -o run --output-format csv -- python3 bench.py $HB
 run B_fetch 200 rocprofv3 --pmc FETCH_SIZE -d $R/$O/B/fetch -o run --output-format csv -- python3 bench.py $HB
 run B_write 200 rocprofv3 --pmc WRITE_SIZE -d $R/$O/B/write -o run --output-format csv -- python3 bench.py $HB
