@@ -380,7 +380,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--global-batch", type=int, default=65536,
                     help="instances over all GPUs (strong scaling: split over the ranks)")
     ap.add_argument("--weak-batch", type=int, default=65536,
