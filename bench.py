@@ -41,6 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "mpc-limx-control_amd"))
 
 FP64_PEAK_TFLOPS = 78.6  # MI355X dense FP64 (vector = matrix), AMD spec; SURVEY.md 8d
+HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E (/opt/skills/guides/MI355X_MICROARCH.md)
 METRIC = "QP solves/sec, 13-state N=10 SRBM MPC, batch=65536 at 1/2/4/8 MI355X"
 CANDIDATES = 16  # gait candidates per state: shards are aligned to whole states
 
@@ -77,8 +78,26 @@ def config_bytes(p):
 
 
 def flops_per_qp(p, mean_iters):
+    """SURVEY.md 8d's count (the reference's dense path), per QP"""
     fl = algorithmic_flops(p["nx"], p["nu"], p["N"])
     return fl["condense"] + fl["solve_fixed"] + fl["per_iter"] * float(mean_iters)
+
+
+def closed_form_work(p, contact, iters, max_nf):
+    """-> (flops, instances) of the closed-form path's own algorithmic count (mpcqp.flops) over
+    the instances the one-wave kernel solved (nf <= max_nf; the rest are the overflow kernel's)"""
+    from mpcqp import flops
+    return flops.batch_flops(p, contact, iters, max_nf=max_nf)
+
+
+def hbm_fields(traffic, kernel_ms, alg_bytes):
+    """HBM rate of the measured traffic (PMC bytes per launch) against the 8 TB/s peak"""
+    if not traffic:
+        return dict(hbm_gbps=None, hbm_frac=None)
+    gbps = traffic / (kernel_ms * 1e-3) / 1e9
+    return dict(hbm_gbps=gbps, hbm_frac=gbps / HBM_PEAK_GBPS,
+                algorithmic_gbps=alg_bytes / (kernel_ms * 1e-3) / 1e9,
+                traffic_over_algorithmic=traffic / alg_bytes)
 
 
 def _profile_json(name):
@@ -299,15 +318,27 @@ def time_config(config, B, seed, steps=10, warmup=2, gait=None, device=0):
     st = d["status"].cpu().numpy()
     it = d["iters"].cpu().numpy()
     f_qp = flops_per_qp(p, it.mean())
-    ach = f_qp * B / (ms * 1e-3) / 1e12
+    ach8d = f_qp * B / (ms * 1e-3) / 1e12
     out = dict(batch=B, nx=p["nx"], nu=p["nu"], N=p["N"],
                constraints="box+friction" if p["constraints"] else "box",
                gait=gait or "alternating (calculateGait, swing = stance = 0.5 s)",
                R=float(p["R"][0, 0]), kernel=eng.fused_kernel, kernel_ms=ms,
                qps=B / (ms * 1e-3), mean_solver_iters=float(it.mean()),
-               max_solver_iters=int(it.max()), solved_frac=float(np.mean(st == 0)),
-               algorithmic_flops_per_qp=f_qp, achieved_tflops=ach,
-               frac=ach / FP64_PEAK_TFLOPS)
+               max_solver_iters=int(it.max()), solved_frac=float(np.mean(st == 0)))
+    if p["model"] in (0, 1):
+        # closed-form path: its own algorithmic count over every instance of the call (ms is
+        # the whole solve call, overflow launch included)
+        fl, _ = closed_form_work(p, batch["contact"], it, None)
+        out.update(algorithmic_flops_per_qp=fl / B, achieved_tflops=fl / (ms * 1e-3) / 1e12,
+                   frac=fl / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                   flops_basis="closed-form path's algorithmic count (mpcqp/flops.py)",
+                   work_rate_vs_survey_8d=dict(flops_per_qp=f_qp, tflops=ach8d,
+                                               frac=ach8d / FP64_PEAK_TFLOPS))
+    else:
+        # the dense model (config E) runs the reference's algorithm (Pade expm, condensing):
+        # SURVEY.md 8d's count is its count
+        out.update(algorithmic_flops_per_qp=f_qp, achieved_tflops=ach8d,
+                   frac=ach8d / FP64_PEAK_TFLOPS, flops_basis="SURVEY.md 8d")
     ex = _profile_json(f"pmc_flops_{config}.json")
     if ex and ex.get("batch") == B and gait is None:
         # executed FP64 work of this kernel (64 lanes x SQ_INSTS_VALU_FLOPS_FP64 + 512 x MFMA
@@ -316,6 +347,7 @@ def time_config(config, B, seed, steps=10, warmup=2, gait=None, device=0):
         out["pipe_frac"] = out["executed_tflops"] / FP64_PEAK_TFLOPS
         out["mfma_tflops"] = ex["mfma_flops_per_launch"] / (ms * 1e-3) / 1e12
         out["mfma_busy_frac"] = ex.get("mfma_busy_frac")
+        out["lane_efficiency"] = out["achieved_tflops"] / out["executed_tflops"]
         out["pmc_source"] = f"profiles/pmc_flops_{config}.json ({ex.get('tag')})"
         out["pmc_matches_library"] = ex.get("lib_build_id") == lib_build_id()
     tr = _profile_json(f"pmc_traffic_{config}.json")
@@ -326,6 +358,7 @@ def time_config(config, B, seed, steps=10, warmup=2, gait=None, device=0):
         out["traffic_bytes_per_launch"] = tr["hbm_bytes_per_launch"]
         out["algorithmic_bytes_per_launch"] = alg
         out["traffic_over_algorithmic"] = tr["hbm_bytes_per_launch"] / alg
+        out.update(hbm_fields(tr["hbm_bytes_per_launch"], ms, alg))
         out["traffic_source"] = f"profiles/pmc_traffic_{config}.json ({tr.get('tag')})"
         out["traffic_matches_library"] = tr.get("lib_build_id") == lib_build_id()
     eng.close()
@@ -438,6 +471,19 @@ def main():
                          "per rank")
     s0, ns = shard(S_total, world, rank)
     i0, B = s0 * CANDIDATES, ns * CANDIDATES
+    # what the process group actually formed, per rank (a SCALE run checks
+    # itself): world size after init, each rank's device and its shard of the global batch
+    me = dict(rank=rank, local_rank=local, device=str(dev), shard=[i0, i0 + B], states=[s0, s0 + ns])
+    if not dry:
+        me["device_name"] = torch.cuda.get_device_name(dev)
+        me["pci_bus_id"] = torch.cuda.get_device_properties(dev).pci_bus_id \
+            if hasattr(torch.cuda.get_device_properties(dev), "pci_bus_id") else None
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
+        formed = dict(backend=dist.get_backend(), world_size=dist.get_world_size(), ranks=ranks)
+    else:
+        formed = dict(backend=None, world_size=1, ranks=[me])
 
     def run_line(batch_local, index_base, steps, warmup, serial=False):
         """time `steps` steps of solve + selection on this rank's shard; returns
@@ -609,6 +655,11 @@ def main():
                 else "step s's all-gather in flight during step s + 1's solve (mpcqp.dist."
                      "PipelinedSelect); every selection completes inside the timed region")
             cfg["serial_select_ms_per_step"] = serial_ms
+            cfg["pipelined_ms_per_step"] = elapsed / args.steps * 1e3
+        cfg["process_group"] = formed
+        covered = sorted(tuple(r["shard"]) for r in formed["ranks"])
+        cfg["shards_cover_global_batch"] = (covered[0][0] == 0 and covered[-1][1] == G and all(
+            a[1] == b[0] for a, b in zip(covered, covered[1:])))
     if rank == 0 and dry:
         cfg["dry_run"] = "selection only: synthetic costs, gloo, no solve"
         out["config"] = cfg
@@ -618,7 +669,10 @@ def main():
         # the dominant kernel's own launches (library events around it); the events around the
         # whole solve in the timed steps (mpc_ms) also hold the overflow launch
         k_ms = kern[eng.fused_kernel]["ms"] if eng.fused_kernel in kern else mpc_ms
-        achieved = f_qp * B / (k_ms * 1e-3) / 1e12
+        # the work of the instances that kernel solved (an overflow instance is the workgroup
+        # kernel's, timed apart): the closed-form path's own algorithmic count
+        fl, n_solved = closed_form_work(p, local_batch["contact"], iters, eng.pair_nf)
+        achieved = fl / (k_ms * 1e-3) / 1e12
         traffic, traffic_tag, traffic_lib = pmc_traffic(args.config, B)
         build = lib_build_id()
         kms = {k: v["ms"] for k, v in kern.items()}
@@ -627,32 +681,44 @@ def main():
         if not fused:
             kms["k_select_min"] = sel_ms
         cfg.update(solved_frac=solved, mean_solver_iters=float(iters.mean()),
+                   max_solver_iters=int(iters.max()),
                    fast_path=eng.fast_path, select=args.select, kernel_ms=kms,
                    kernel_launches={k: v["launches"] for k, v in kern.items()})
+        alg_bytes = algorithmic_bytes(p["nx"], p["nu"], p["N"]) * B
         roof = dict(bound="fp64-valu", compute_unit="fp64 VALU (k_mpc_pair issues no MFMA)",
                     kernel=eng.fused_kernel, kernel_ms=k_ms, achieved=achieved,
-                    peak=FP64_PEAK_TFLOPS,
-                    unit="TFLOP/s", frac=achieved / FP64_PEAK_TFLOPS, traffic=traffic,
+                    peak=FP64_PEAK_TFLOPS, unit="TFLOP/s", frac=achieved / FP64_PEAK_TFLOPS,
+                    traffic=traffic,
+                    flops_basis="closed-form path's own algorithmic count (mpcqp/flops.py, "
+                                "DESIGN.md section 4 'Roofline accounting'): model, S blocks, "
+                                "u/v, gradient, H_FF, nf^3/3 Cholesky + nf^3/3 inverse, "
+                                "per-pass dual flops x each instance's passes",
+                    algorithmic_flops_per_qp=fl / max(1, n_solved), instances=n_solved,
+                    work_rate_vs_survey_8d=dict(
+                        flops_per_qp=f_qp, tflops=f_qp * B / (k_ms * 1e-3) / 1e12,
+                        frac=f_qp * B / (k_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                        note="SURVEY.md 8d prices the reference's dense path (expm, powers, "
+                             "Phi chain, B'QB); the closed form does not execute it, so this "
+                             "is a work rate, not a roofline fraction"),
                     traffic_source=(f"profiles/{traffic_tag}_summary.json (rocprofv3 PMC, "
                                     "2 x FETCH_SIZE + WRITE_SIZE)") if traffic else None,
                     traffic_lib_build_id=traffic_lib, lib_build_id=build,
                     traffic_matches_library=(traffic_lib == build) if traffic else None,
-                    algorithmic_bytes_per_launch=algorithmic_bytes(p["nx"], p["nu"], p["N"]) * B,
-                    algorithmic_flops_per_qp=f_qp,
-                    basis="SURVEY.md 8d algorithmic flops (F_fixed + F_iter x mean iters) per "
-                          "QP x batch / fused-kernel time; the closed-form path executes "
-                          "fewer, so frac is a work rate, not pipe utilisation (see "
-                          "executed_tflops / pipe_frac)",
-                    whole_step_tflops=f_qp * B / (ms_per_step * 1e-3) / 1e12)
+                    algorithmic_bytes_per_launch=alg_bytes,
+                    mfma_busy_frac=None)
+        roof.update(hbm_fields(traffic, k_ms, alg_bytes))
         ex = pmc_executed(args.config, B)
         if ex:
             per_launch = ex["executed_flops_per_launch"]
             roof["executed_tflops"] = per_launch / (k_ms * 1e-3) / 1e12
             roof["pipe_frac"] = roof["executed_tflops"] / FP64_PEAK_TFLOPS
+            roof["lane_efficiency"] = achieved / roof["executed_tflops"]
+            roof["mfma_busy_frac"] = ex.get("mfma_busy_frac")
             roof["executed_source"] = f"profiles/{ex.get('file', 'pmc_flops.json')} " \
                                       "(64 lanes x SQ_INSTS_VALU_FLOPS_FP64, a per-wave-" \
                                       "instruction count: EXEC-masked lanes included, an " \
-                                      "upper bound; + MFMA ops)"
+                                      "upper bound; + MFMA ops; SQ_VALU_MFMA_BUSY_CYCLES for " \
+                                      "mfma_busy_frac)"
             roof["executed_tag"] = ex.get("tag")
             roof["executed_matches_library"] = ex.get("lib_build_id") == build
         out["roofline"] = roof

@@ -177,6 +177,10 @@ int mpcqp_ctx_reserve(mpcqp_ctx *ctx, int B);
  * P); 2 when it runs the fused kernel with two QPs per wavefront (N = 10, box bounds,
  * max_free <= 30: config B and the literal 13/3/10) */
 int mpcqp_ctx_fast_path(const mpcqp_ctx *ctx);
+/* free variables the one-wave fused kernel holds per instance (30 for the paired kernel, its NF
+ * otherwise; 0 on the generic path): an instance with more goes to the overflow workgroup kernel
+ * (bench.py counts the one-wave kernel's work over the instances it solved) */
+int mpcqp_ctx_one_wave_nf(const mpcqp_ctx *ctx);
 
 /* Staged entry points (stage 1 / stage 2 below, mpcqp_batch_solve_qp): the stand-alone solve
  * holds 64 free variables per instance (more: per-instance status MPCQP_ERR_BAD_DIMS).  On a
@@ -293,7 +297,10 @@ int mpcqp_kf_update(void *stream, int R, double dt, double *xhat, double *P, con
  * (which = 1: condense_solve / generic solve; the whole mpcqp_batch_solve) launch, HIP events on
  * the ctx stream (ms; -1 if none recorded).  On the fused path which = 2 times the one-wave kernel
  * alone (k_mpc_pair / k_mpc) and which = 3 the overflow workgroup kernel (k_mpc_wg) launched
- * after it.  Timing is off until enabled. */
+ * after it.  Timing is off until enabled.  mpcqp_batch_solve_host does not feed these slots: its
+ * step is replayed as a captured HIP graph, and an event record inside the capture would time the
+ * capture, not the replay.  mpcqp_enable_timing creates its events all at once (none are kept if
+ * one creation fails). */
 int mpcqp_enable_timing(mpcqp_ctx *ctx, int on);
 double mpcqp_last_kernel_ms(mpcqp_ctx *ctx, int which);
 /* sum (ms) over the launches of slot `which` recorded since the previous call (at most the last

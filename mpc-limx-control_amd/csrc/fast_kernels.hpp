@@ -7,6 +7,10 @@
 
 #include "../../include/mpcqp.h"
 
+#ifdef MPCQP_VARIANT_TAG  // set only on a variant build's translation unit (build_variants.sh)
+extern "C" const char *mpcqp_variant_tag_fn(void) { return MPCQP_VARIANT_TAG; }
+#endif
+
 #ifndef MPCQP_W32
 #define MPCQP_W32 3  // waves per SIMD the NF <= 32 fused kernel is register-budgeted for
 #endif

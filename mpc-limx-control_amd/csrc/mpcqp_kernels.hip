@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -541,7 +542,10 @@ struct mpcqp_ctx {
     int wg_grid = 0;                        // resident workgroups of the workgroup kernel
     // host-pointer entry point (mpcqp_batch_solve_host): device staging, pinned host staging of
     // the same byte layout (one copy each way), its own stream (graph capture needs one) and
-    // the instantiated graphs of the last batch size (one per overflow-list parity)
+    // the instantiated graphs of the last batch size: [0] no overflow launch, [1 + parity] with
+    // the overflow launch on list `parity`.  A graph holds the device addresses it was captured
+    // with (staging, overflow lists, scratch): every reallocation of a context-owned device
+    // buffer bumps buf_gen, and graphs captured under an older generation are dropped
     void *hbuf = nullptr;
     size_t hbuf_cap = 0;
     void *pin = nullptr;
@@ -549,8 +553,8 @@ struct mpcqp_ctx {
     hipStream_t hstream = nullptr;
     hipEvent_t hev = nullptr;
     int hg_B = 0;
-    bool hg_ovf = false;
-    hipGraphExec_t hg_exec[2] = {nullptr, nullptr};
+    unsigned long long buf_gen = 0, hg_gen = 0;
+    hipGraphExec_t hg_exec[3] = {nullptr, nullptr, nullptr};
     bool hg_off = false;  // capture failed once: run the host path uncaptured
     // closed-loop rollout workspace
     void *rbuf = nullptr;
@@ -567,7 +571,19 @@ extern "C" {
 #ifndef MPCQP_BUILD_ID
 #define MPCQP_BUILD_ID "unversioned"
 #endif
-const char *mpcqp_build_id(void) { return MPCQP_BUILD_ID; }
+// A/B variant builds (tools/build_variants.sh) recompile one translation unit with extra -D
+// flags and relink it with the release objects; that unit then defines the strong
+// mpcqp_variant_tag_fn (fast_kernels.hpp), so the id of a variant library names its flags
+__attribute__((weak)) const char *mpcqp_variant_tag_fn(void) { return ""; }
+
+const char *mpcqp_build_id(void) {
+    static char id[96];
+    if (!id[0]) {
+        const char *v = mpcqp_variant_tag_fn();
+        snprintf(id, sizeof id, "%s%s%s", MPCQP_BUILD_ID, v[0] ? "+" : "", v);
+    }
+    return id;
+}
 
 const char *mpcqp_status_string(int s) {
     switch (s) {
@@ -790,8 +806,8 @@ out:
 // ------------------------------------------------------------------------- batched path
 // F (n x n, column-major) with M = F F' for a symmetric positive semi-definite M: the square
 // roots of a diagonal M, otherwise cyclic Jacobi M = V L V' and F = V L^(1/2).  false if M is
-// not symmetric or has an eigenvalue below -1e-12 max |eigenvalue| (the dense kernel then keeps
-// the recursion, which takes any Q and P)
+// not symmetric, has an eigenvalue below -1e-12 max |eigenvalue| or Jacobi does not converge
+// (the dense kernel then keeps the recursion, which takes any Q and P)
 static bool sym_factor(const double *M, int n, double *F) {
     double mx = 0.0;
     for (int i = 0; i < n * n; ++i) mx = std::max(mx, std::fabs(M[i]));
@@ -805,11 +821,13 @@ static bool sym_factor(const double *M, int n, double *F) {
     std::vector<double> A(M, M + (size_t)n * n), V((size_t)n * n, 0.0);
     for (int i = 0; i < n; ++i) V[(size_t)i * n + i] = 1.0;
     if (!diag) {
-        for (int sweep = 0; sweep < 64; ++sweep) {
+        bool converged = false;
+        for (int sweep = 0; sweep <= 64 && !converged; ++sweep) {
             double off = 0.0;
             for (int q = 0; q < n; ++q)
                 for (int p = 0; p < q; ++p) off += A[(size_t)q * n + p] * A[(size_t)q * n + p];
-            if (off <= 1e-32 * mx * mx) break;
+            if (off <= 1e-32 * mx * mx) { converged = true; break; }
+            if (sweep == 64) break;  // (the off-diagonal test of the 64th sweep's result)
             for (int q = 1; q < n; ++q)
                 for (int p = 0; p < q; ++p) {
                     const double apq = A[(size_t)q * n + p];
@@ -835,6 +853,9 @@ static bool sym_factor(const double *M, int n, double *F) {
                     }
                 }
         }
+        // not diagonalised to the tolerance in 64 sweeps: F F' would not be M -- keep the
+        // recursion path, which takes any Q and P
+        if (!converged) return false;
     }
     double lmax = 0.0;
     for (int i = 0; i < n; ++i) lmax = std::max(lmax, std::fabs(A[(size_t)i * n + i]));
@@ -954,6 +975,11 @@ int mpcqp_ctx_fast_path(const mpcqp_ctx *c) {
     return c->fk.pair ? 2 : 1;
 }
 
+int mpcqp_ctx_one_wave_nf(const mpcqp_ctx *c) {
+    if (!c || !c->fast || c->fk.dense) return 0;
+    return c->fk.prim_nf;
+}
+
 int mpcqp_debug_phase_cycles(mpcqp_ctx *c, uint64_t *out, int n) {
 #ifdef MPCQP_STAMPS
     if (!c || !out || n <= 0) return MPCQP_ERR_BAD_ARG;
@@ -994,7 +1020,7 @@ int mpcqp_ctx_destroy(mpcqp_ctx *c) {
     hipFree(c->dsel);
     hipFree(c->dlist);
     hipFree(c->hbuf);
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 3; ++i)
         if (c->hg_exec[i]) hipGraphExecDestroy(c->hg_exec[i]);
     if (c->pin) hipHostFree(c->pin);
     if (c->hev) hipEventDestroy(c->hev);
@@ -1033,12 +1059,13 @@ int mpcqp_enable_timing(mpcqp_ctx *c, int on) {
     if (!c) return MPCQP_ERR_BAD_ARG;
     if (on && !c->ev_ok) {
         hipSetDevice(c->device);
-        bool ok = true;
-        for (int w = 0; w < 4; ++w)
-            for (int i = 0; i < mpcqp_ctx::kTimingRing; ++i)
-                for (int e = 0; e < 2; ++e)
-                    if (hipEventCreate(&c->ev[w][i][e]) != hipSuccess) ok = false;
-        if (!ok) return MPCQP_ERR_DEVICE;
+        hipEvent_t *evs = &c->ev[0][0][0];
+        constexpr int nev = 4 * mpcqp_ctx::kTimingRing * 2;
+        for (int i = 0; i < nev; ++i)
+            if (hipEventCreate(&evs[i]) != hipSuccess) {
+                for (int j = 0; j < i; ++j) hipEventDestroy(evs[j]);  // no partial set is kept
+                return MPCQP_ERR_DEVICE;
+            }
         c->ev_ok = true;
     }
     c->timing = on && c->ev_ok;
@@ -1167,6 +1194,7 @@ static int ensure_bytes(mpcqp_ctx *c, void **buf, size_t *cap, size_t bytes) {
     hipFree(*buf);
     *buf = nullptr;
     *cap = 0;
+    ++c->buf_gen;  // captured host-path graphs may hold the old address
     if (hipMalloc(buf, bytes) != hipSuccess) return MPCQP_ERR_DEVICE;
     *cap = bytes;
     return MPCQP_OK;
@@ -1212,6 +1240,7 @@ static int ensure_list(mpcqp_ctx *c, int B) {
     hipFree(c->dlist);
     c->dlist = nullptr;
     c->list_cap = 0;
+    ++c->buf_gen;
     const size_t stride = list_stride((size_t)B);
     if (hipMalloc(&c->dlist, sizeof(int) * 2 * stride) != hipSuccess ||
         hipMemsetAsync(c->dlist, 0, sizeof(int) * kListHeadWords, c->stream) != hipSuccess ||
@@ -1359,6 +1388,7 @@ static int ensure_scratch_hf(mpcqp_ctx *c, int B) {
     hipFree(c->scratchF);
     c->scratchH = c->scratchF = nullptr;
     c->scratch_cap = 0;
+    ++c->buf_gen;
     if (hipMalloc(&c->scratchH, sizeof(double) * nV * nV * B) != hipSuccess ||
         hipMalloc(&c->scratchF, sizeof(double) * nV * B) != hipSuccess)
         return MPCQP_ERR_DEVICE;
@@ -1565,7 +1595,7 @@ static int host_step(mpcqp_ctx *c, int B, bool ovf, size_t in_bytes, size_t out_
 }
 
 static void host_graphs_drop(mpcqp_ctx *c) {
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 3; ++i)
         if (c->hg_exec[i]) { hipGraphExecDestroy(c->hg_exec[i]); c->hg_exec[i] = nullptr; }
     c->hg_B = 0;
 }
@@ -1588,18 +1618,16 @@ int mpcqp_batch_solve_host(mpcqp_ctx *c, int B, const double *x0, const double *
     const size_t out_off = (in_bytes + 15) & ~(size_t)15;
     const size_t b_u = sizeof(double) * nV * B, b_c = sizeof(double) * B, b_i = sizeof(int) * B;
     const size_t out_bytes = b_u + b_c + 2 * b_i, total = out_off + out_bytes;
-    const void *hb = c->hbuf;
     if (ensure_bytes(c, &c->hbuf, &c->hbuf_cap, std::max(total, host_stage_bytes(c, B))))
         return MPCQP_ERR_DEVICE;
     if (c->pin_cap < total) {
         if (c->pin) hipHostFree(c->pin);
         c->pin = nullptr;
         c->pin_cap = 0;
+        ++c->buf_gen;
         if (hipHostMalloc(&c->pin, total, hipHostMallocDefault) != hipSuccess) return MPCQP_ERR_DEVICE;
         c->pin_cap = total;
-        host_graphs_drop(c);
     }
-    if (c->hbuf != hb) host_graphs_drop(c);
     if (!c->hstream) {
         if (hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&c->hev, hipEventDisableTiming) != hipSuccess)
@@ -1607,6 +1635,12 @@ int mpcqp_batch_solve_host(mpcqp_ctx *c, int B, const double *x0, const double *
     }
     const bool ovf = host_may_overflow(c, B, contact);
     if (ovf && ensure_list(c, B)) return MPCQP_ERR_DEVICE;  // (allocates outside any capture)
+    // (after every allocation this call may make: a graph is captured against the buffers as
+    // they are now)
+    if (c->hg_gen != c->buf_gen) {
+        host_graphs_drop(c);
+        c->hg_gen = c->buf_gen;
+    }
     char *h = (char *)c->pin;
     memcpy(h, x0, b_x0);
     memcpy(h + b_x0, xref, b_xr);
@@ -1619,12 +1653,13 @@ int mpcqp_batch_solve_host(mpcqp_ctx *c, int B, const double *x0, const double *
     int rc = MPCQP_OK;
     const bool graph = c->fast && !c->hg_off;
     if (graph) {
-        if (c->hg_B != B || c->hg_ovf != ovf) {
+        if (c->hg_B != B) {
             host_graphs_drop(c);
             c->hg_B = B;
-            c->hg_ovf = ovf;
         }
-        const int par = ovf ? c->list_par : 0;
+        // one graph per (overflow launch, list parity): a contact schedule that flips the
+        // overflow prediction from tick to tick replays cached graphs instead of re-capturing
+        const int par = ovf ? 1 + c->list_par : 0;
         if (!c->hg_exec[par]) {
             // capture one call's stream work; the capture does not run it, so the list parity
             // the capture advanced is put back (the launch below advances it)
@@ -1634,7 +1669,7 @@ int mpcqp_batch_solve_host(mpcqp_ctx *c, int B, const double *x0, const double *
             bool ok = hipStreamBeginCapture(c->hstream, hipStreamCaptureModeThreadLocal) == hipSuccess;
             const int rcc = ok ? host_step(c, B, ovf, in_bytes, out_off, out_bytes, b_ct != 0) : MPCQP_OK;
             if (ok) ok = hipStreamEndCapture(c->hstream, &g) == hipSuccess && rcc == MPCQP_OK;
-            c->list_par = ovf ? par : c->list_par;
+            c->list_par = ovf ? par - 1 : c->list_par;
             c->timing = timing;
             if (ok) ok = hipGraphInstantiate(&c->hg_exec[par], g, nullptr, nullptr, 0) == hipSuccess;
             if (g) hipGraphDestroy(g);

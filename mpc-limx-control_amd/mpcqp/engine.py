@@ -94,6 +94,12 @@ class BatchEngine:
         return bool(lib().mpcqp_ctx_fast_path(self.ctx))
 
     @property
+    def pair_nf(self) -> int:
+        """free variables per instance the one-wave fused kernel solves (more: the overflow
+        workgroup kernel)"""
+        return int(lib().mpcqp_ctx_one_wave_nf(self.ctx))
+
+    @property
     def fused_kernel(self) -> str:
         """name of the kernel mpcqp_batch_solve launches: k_mpc_pair (two QPs per wave),
         k_mpc (one QP per wave) or the generic k_condense + k_solve pair"""

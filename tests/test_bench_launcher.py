@@ -28,13 +28,14 @@ def _run(world, G, seed=11):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("world", [1, 2])
-def test_bench_launcher_global_argmin(world):
+@pytest.mark.parametrize("world,G", [(1, 4096), (2, 4096), (3, 4097 * 16)])
+def test_bench_launcher_global_argmin(world, G):
+    """(3, 4097 x 16): an uneven state split, 1366 / 1366 / 1365 states over three ranks"""
     sys.path.insert(0, ROOT)
     import bench
     from mpcqp.dist import host_select
 
-    G, seed = 4096, 11
+    seed = 11
     r = _run(world, G, seed)
     assert r["n_gpus"] == world
     assert r["scaling"] == "strong" and r["config"]["global_batch"] == G
@@ -55,3 +56,20 @@ def test_shards_cover_whole_states():
             s0, n = bench.shard(S, w, r)
             cover.extend(range(s0, s0 + n))
         assert cover == list(range(S))
+
+
+def test_bench_line_records_the_formed_group():
+    """the line names the world size the process group formed, each rank's
+    device and shard, and both the pipelined and the serial-selection step times"""
+    r = _run(2, 4096)
+    cfg = r["config"]
+    pg = cfg["process_group"]
+    assert pg["world_size"] == 2 and pg["backend"] == "gloo"
+    ranks = sorted(pg["ranks"], key=lambda x: x["rank"])
+    assert [x["rank"] for x in ranks] == [0, 1]
+    assert [x["local_rank"] for x in ranks] == [0, 1]
+    assert all(x["device"] == "cpu" for x in ranks)  # dry run; cuda:<local_rank> on the GPU box
+    assert ranks[0]["shard"] == [0, 2048] and ranks[1]["shard"] == [2048, 4096]
+    assert cfg["shards_cover_global_batch"] is True
+    assert cfg["pipelined_ms_per_step"] == pytest.approx(r["ms_per_step"])
+    assert cfg["serial_select_ms_per_step"] > 0

@@ -86,3 +86,48 @@ def test_host_tick_batch_size_change(gpu):
         b = mpcqp.make_batch(p, B, seed=B)
         same(host_solve(eng, p, b), device_solve(eng, b))
     eng.close()
+
+
+def test_host_graph_survives_buffer_reallocation(gpu):
+    """a host-path graph holds the overflow-list and staging addresses it was
+    captured with; a device solve at a larger batch (or mpcqp_ctx_reserve) reallocates them.
+    Host tick B = 16 on a mixed gait -> device solve B = 4,096 (grows the lists) -> host tick
+    B = 16 again must re-capture, not replay against freed memory"""
+    import mpcqp
+    from mpcqp._lib import lib
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("B")
+    b16 = mpcqp.make_batch(p, 16, seed=5, gait="mixed")
+    big = mpcqp.make_batch(p, 4096, seed=6, gait="mixed")
+    eng = BatchEngine(p)
+    ref16 = device_solve(eng, b16)
+    same(host_solve(eng, p, b16), ref16)
+    ref_big = device_solve(eng, big)  # grows the overflow lists past the captured ones
+    for _ in range(3):
+        same(host_solve(eng, p, b16), ref16)
+    assert lib().mpcqp_ctx_reserve(eng.ctx, 8192) == 0  # grows the host staging too
+    for _ in range(3):
+        same(host_solve(eng, p, b16), ref16)
+    same(device_solve(eng, big), ref_big)
+    eng.close()
+
+
+def test_host_tick_overflow_flips(gpu):
+    """ADVICE r03 (medium): a walking schedule flips the overflow prediction from tick to tick;
+    the graphs for (no overflow) and (overflow, list parity 0 / 1) are cached side by side and
+    every tick still equals the device path"""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("B")
+    mixed = mpcqp.make_batch(p, 16, seed=7, gait="mixed")
+    alt = mpcqp.make_batch(p, 16, seed=7)
+    nf_alt = np.array([3 * bin(int(c)).count("1") for c in alt["contact"]])
+    assert (nf_alt <= 30).all()
+    eng = BatchEngine(p)
+    ref_m, ref_a = device_solve(eng, mixed), device_solve(eng, alt)
+    for i in range(8):
+        if i % 3 == 2:
+            same(host_solve(eng, p, alt), ref_a)
+        else:
+            same(host_solve(eng, p, mixed), ref_m)
+    eng.close()

@@ -10,6 +10,8 @@ cd "$R/mpc-limx-control_amd" || exit 1
 HF="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -w -mllvm -pragma-unroll-threshold=1000000 -mllvm -amdgpu-sched-strategy=max-ilp"
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
+  # the variant's flags go into mpcqp_build_id() (PMC summaries of variants stay distinct)
+  flags="$flags -DMPCQP_VARIANT_TAG=\"$name-$(echo "$TU $flags" | sha1sum | cut -c1-8)\""
   ( mkdir -p "build/$name" && /opt/rocm/bin/hipcc $HF $flags -c -o "build/$name/$TU.o" csrc/$TU.hip && \
     /opt/rocm/bin/hipcc $HF -shared -o "lib/libmpcqp_$name.so" $(ls build/rel/*.o | grep -v $TU.o) \
         "build/$name/$TU.o" && \
