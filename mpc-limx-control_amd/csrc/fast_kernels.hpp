@@ -38,6 +38,7 @@ struct FastKernels {
     int nx = 0, nu = 0;
     int prim_nf = 0;  // free variables the one-wave kernel holds (kPairCap or its NF)
     int nf = 0;       // NF the one-wave kernel is instantiated for
+    int crash_k = 0, crash_p = 0;  // the one-wave kernel's crash start (0: none)
 };
 
 constexpr int kPairCap = 30;  // free variables of one half of the paired kernel (mpc_pair.hpp)

@@ -26,6 +26,8 @@ void add_pair(FastKernels &k) {
     k.pair = (const void *)&k_mpc_pair<NU, N, MODEL, false>;
     if constexpr (MODEL == 0) k.pair_gen = (const void *)&k_mpc_pair<NU, N, MODEL, true>;
     k.pair_lds = PairLayout<NU, N, MODEL>::lds_bytes;
+    k.crash_k = MPCQP_PAIR_CRASH ? kPairCrashK : 0;
+    k.crash_p = MPCQP_PAIR_CRASH ? kPairCrashP : 0;
 }
 
 }  // namespace

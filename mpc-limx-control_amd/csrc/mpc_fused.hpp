@@ -45,6 +45,7 @@ struct MpcArgs {
     const double *rmat;     // R, nu x nu column-major (device)
     double fz_min, fz_max, fxy_max, u_min, u_max, mu;
     int max_iter, max_free;
+    int crash_p;  // paired kernel: working sets of its crash start before the dual loop (0: none)
     const double *lin, *x0, *xref;
     const uint64_t *contact;
     double *U, *cost;

@@ -55,8 +55,21 @@ namespace mpcqp {
 #ifndef MPCQP_PAIR_RINV
 #define MPCQP_PAIR_RINV 1
 #endif
+// speculative primal-dual active-set start before the dual loop (see the crash block below);
+// 0 = plain Goldfarb-Idnani from the unconstrained minimum (A/B builds)
+#ifndef MPCQP_PAIR_CRASH
+#define MPCQP_PAIR_CRASH 1
+#endif
 
 constexpr int kPairNF = 30;  // free variables per instance; lane 31 of a half carries g
+// crash start (below): bounds per working set, working sets before giving up
+#ifndef MPCQP_CRASH_K
+#define MPCQP_CRASH_K 15
+#endif
+#ifndef MPCQP_CRASH_P
+#define MPCQP_CRASH_P 8
+#endif
+constexpr int kPairCrashK = MPCQP_CRASH_K, kPairCrashP = MPCQP_CRASH_P;
 
 template <int NU, int N, int MODEL>
 struct PairLayout {
@@ -685,6 +698,140 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         const double blo = blo_of(stb), bhi = bhi_of(stb);  // (bit 2 of stb never changes)
         const double tlo = -kFeasTol * (1.0 + fabs(blo)), thi = -kFeasTol * (1.0 + fabs(bhi));
         bool done = !ok2;
+#if MPCQP_PAIR_CRASH
+        // ---- crash: speculative primal-dual active-set start (oracle box_crash, DESIGN.md
+        //      section 4).  Working set A = every bound the unconstrained minimum x0 violates
+        //      (at most KC: the bounds already in A, then the lowest variable ids); with A's
+        //      bounds as equalities the minimiser is x = x0 - J J_A' w, M w = x0_A - b_A,
+        //      M = J_A J_A' = (H^-1)_AA.  Lane a of A publishes its J row (LDS, the dead L space),
+        //      computes row rank(a) of M against the published rows, and the k x k system is
+        //      solved by Gauss-Jordan, one pivot row broadcast per step.  The next A drops
+        //      negative multipliers (lambda_a = -side_a w_a) and adds what x violates; an
+        //      unchanged A is the optimum (the strictly convex QP's KKT point, within the dual
+        //      loop's own tolerances), and the half skips the dual loop.  After PC working sets
+        //      or a non-positive pivot the half gives up with J, x0 and f0 untouched and runs
+        //      Goldfarb-Idnani as before.  Iterations = the working sets that needed a solve.
+        //      One wavefront loop for both halves; every ballot runs with all lanes active.
+        {
+            constexpr int KC = kPairCrashK;
+            const int PC = a.crash_p;
+            static_assert(KC * NF <= Lay::NR, "the published J rows fit the dead L space");
+            static_assert(KC + 2 <= NP, "the pivot row fits the row buffer");
+            double *Wr = D + Lay::oR;             // [KC][NF] published J rows
+            double *Pv = rowbuf;                  // pivot row [KC], its r, 1 / pivot
+            double *Wv = colb;                    // w by rank
+            double *Yv = rot;                     // y = J_A' w [NF]
+            const double x0v = x, f0 = fval;
+            double xc = x0v, lam = 0.0, fc = f0;
+            int side = 0, cit = 0;
+            bool crashing = !done, cok = false;
+            while (__ballot(crashing) != 0ull) {
+                int nw = side;
+                if (crashing && hl < nf) {
+                    if (side == 0) {
+                        if ((stb & 1) && xc - blo < tlo) nw = 1;
+                        else if ((stb & 2) && -xc - bhi < thi) nw = -1;
+                    } else if (lam < 0.0) {
+                        nw = 0;
+                    }
+                }
+                const bool changed = half_ballot(nw != side) != 0u;
+                if (crashing && !changed) { cok = true; crashing = false; }  // (cit = 0: x0 is optimal)
+                if (crashing && cit >= PC) crashing = false;  // give up
+                {   // at most KC bounds: those already in A, then the lowest variable ids
+                    const uint32_t am = half_ballot(crashing && nw != 0);
+                    const uint32_t km = half_ballot(crashing && nw != 0 && side != 0);
+                    const uint32_t nm = half_ballot(crashing && nw != 0 && side == 0);
+                    const int room = KC - __popc(km);
+                    if (__popc(am) > KC && nw != 0 && side == 0 &&
+                        __popc(nm & ((1u << hl) - 1u)) >= room)
+                        nw = 0;
+                }
+                if (crashing) { side = nw; ++cit; }
+                const uint32_t amask = half_ballot(crashing && side != 0);
+                const int k = __popc(amask);
+                const int rho = __popc(amask & ((1u << hl) - 1u));
+                const bool solving = crashing && k > 0;
+                const bool inA = solving && side != 0;
+                if (crashing && k == 0) { xc = x0v; lam = 0.0; fc = f0; }
+                if (solving) ++iters;
+                const int ks = solving ? k : 0;
+                const int kmax = max(__builtin_amdgcn_readlane(ks, 0), __builtin_amdgcn_readlane(ks, kHalf));
+                if (kmax == 0) continue;  // (wave-uniform)
+                const double bval = side > 0 ? blo : -bhi;
+                const double r0 = x0v - bval;
+                double rr = r0;
+                if (inA) {
+        #pragma unroll
+                    for (int c = 0; c < NF; ++c) Wr[rho * NF + c] = Jr[c];
+                }
+                wave_sync();
+                // row rank(a) of M = J_A J_A' (lane a's own J row against the published rows)
+                double Mr[KC];
+        #pragma unroll
+                for (int m = 0; m < KC; ++m) {
+                    Mr[m] = 0.0;
+                    if (m < kmax) {
+                        double s4[4] = {0.0, 0.0, 0.0, 0.0};
+        #pragma unroll
+                        for (int c = 0; c < NF; ++c) s4[c & 3] += Jr[c] * Wr[m * NF + c];
+                        Mr[m] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+                    }
+                }
+                // Gauss-Jordan without pivoting (M is positive definite): step j's pivot row is
+                // published by the lane of rank j, every other lane of A eliminates column j
+                double dd = 1.0;
+                bool bad = false;
+        #pragma unroll
+                for (int j = 0; j < KC; ++j) {
+                    if (j < kmax) {
+                        if (inA && rho == j) {
+        #pragma unroll
+                            for (int m = j; m < KC; ++m) Pv[m] = Mr[m];
+                            Pv[KC] = rr;
+                            Pv[KC + 1] = 1.0 / Mr[j];
+                            dd = Mr[j];
+                            bad |= !(Mr[j] > 0.0);
+                        }
+                        wave_sync();
+                        if (inA && rho != j && j < k) {
+                            const double l = Mr[j] * Pv[KC + 1];
+        #pragma unroll
+                            for (int m = j + 1; m < KC; ++m) Mr[m] -= l * Pv[m];
+                            rr -= l * Pv[KC];
+                        }
+                        wave_sync();
+                    }
+                }
+                const bool gave_up = half_ballot(bad) != 0u;
+                const double w = inA ? rr / dd : 0.0;
+                if (inA) Wv[rho] = w;
+                wave_sync();
+                // y = J_A' w (lane c: column c of the published rows), then x = x0 - J y
+                double y = 0.0;
+                for (int m = 0; m < kmax; ++m) y += (m < k ? Wr[m * NF + (hl < NF ? hl : 0)] * Wv[m] : 0.0);
+                if (hl < NF) Yv[hl] = y;
+                wave_sync();
+                double s4[4] = {0.0, 0.0, 0.0, 0.0};
+        #pragma unroll
+                for (int c = 0; c < NF; ++c) s4[c & 3] += Jr[c] * Yv[c];
+                const double wr = half_sum(inA ? w * r0 : 0.0);
+                wave_sync();
+                if (solving && !gave_up) {
+                    xc = hl < nf ? x0v - ((s4[0] + s4[1]) + (s4[2] + s4[3])) : 0.0;
+                    if (inA) xc = bval;
+                    lam = inA ? -(double)side * w : 0.0;
+                    fc = f0 + 0.5 * wr;
+                }
+                if (solving && gave_up) crashing = false;
+            }
+            if (cok) {  // this half is solved: the dual loop skips it
+                x = xc;
+                fval = fc;
+                done = true;
+            }
+        }
+#endif
         bool fresh = true;
         int p = 0;
         // the partial multiplier of the constraint being added (slot q), in every lane of the half

@@ -444,6 +444,10 @@ bool pick_fast(int model, int nx, int nu, int N, bool fric, int nfmax, FastKerne
     }
     if (model == MPCQP_MODEL_LITERAL && nu == 3 && !fric) found = pick_fast_literal(N, nprim, k);
     if (found && pair_enabled()) add_fast_pair(model, N, fric, nprim, k);
+    // MPCQP_CRASH_P=n in the environment: the paired kernel's crash start gives up after n
+    // working sets (0: the plain dual loop from the unconstrained minimum; A/B runs and tests)
+    if (k.pair && k.crash_k > 0)
+        if (const char *e = getenv("MPCQP_CRASH_P")) k.crash_p = std::max(0, atoi(e));
     if (found) {
         k.prim_nf = k.pair ? kPairCap : k.nf;
         if (nfmax > k.prim_nf) add_fast_wg(model, N, fric, k);
@@ -980,6 +984,14 @@ int mpcqp_ctx_one_wave_nf(const mpcqp_ctx *c) {
     return c->fk.prim_nf;
 }
 
+int mpcqp_ctx_crash_params(const mpcqp_ctx *c, int *kmax, int *pmax) {
+    if (!c || !kmax || !pmax) return MPCQP_ERR_BAD_ARG;
+    const bool on = c->fast && c->fk.pair && !c->fk.dense;
+    *kmax = on ? c->fk.crash_k : 0;
+    *pmax = on ? c->fk.crash_p : 0;
+    return MPCQP_OK;
+}
+
 int mpcqp_debug_phase_cycles(mpcqp_ctx *c, uint64_t *out, int n) {
 #ifdef MPCQP_STAMPS
     if (!c || !out || n <= 0) return MPCQP_ERR_BAD_ARG;
@@ -1173,6 +1185,7 @@ static MpcArgs mpc_args(mpcqp_ctx *c, int B) {
     a.mu = m.mu;
     a.max_iter = m.max_iter;
     a.max_free = m.max_free > 0 ? m.max_free : m.nu * m.N;
+    a.crash_p = c->fk.crash_p;
     a.stamps = c->dstamps;
     a.cut = 0;
 #ifdef MPCQP_CUTS

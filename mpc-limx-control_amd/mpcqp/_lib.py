@@ -24,7 +24,7 @@ EXPORTS = [
     "mpcqp_discretize", "mpcqp_discretize_quadrature", "mpcqp_build_qp", "mpcqp_solve_dense", "mpcqp_plant_step",
     "mpcqp_ctx_create", "mpcqp_ctx_destroy", "mpcqp_set_stream", "mpcqp_sync",
     "mpcqp_batch_condense", "mpcqp_batch_solve_qp", "mpcqp_batch_solve",
-    "mpcqp_ctx_fast_path", "mpcqp_ctx_one_wave_nf", "mpcqp_batch_discretize", "mpcqp_batch_condense_solve",
+    "mpcqp_ctx_fast_path", "mpcqp_ctx_one_wave_nf", "mpcqp_ctx_crash_params", "mpcqp_batch_discretize", "mpcqp_batch_condense_solve",
     "mpcqp_debug_phase_cycles", "mpcqp_batch_solve_host",
     "mpcqp_batch_select_min", "mpcqp_batch_select_record", "mpcqp_reduce_records",
     "mpcqp_batch_solve_select",
@@ -80,6 +80,7 @@ def lib():
     L.mpcqp_batch_solve.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp]
     L.mpcqp_ctx_fast_path.argtypes = [vp]
     L.mpcqp_ctx_one_wave_nf.argtypes = [vp]
+    L.mpcqp_ctx_crash_params.argtypes = [vp, vp, vp]
     L.mpcqp_debug_phase_cycles.argtypes = [vp, vp, i]
     L.mpcqp_batch_solve_host.argtypes = [vp, i] + [vp] * 8
     L.mpcqp_batch_discretize.argtypes = [vp, i, vp, vp]

@@ -100,6 +100,16 @@ class BatchEngine:
         return int(lib().mpcqp_ctx_one_wave_nf(self.ctx))
 
     @property
+    def crash(self) -> tuple:
+        """(bounds per working set, working sets) of the one-wave kernel's crash start, (0, 0)
+        if none: the oracle reproduces its iteration counts with p["crash"] set to this"""
+        import ctypes as C
+        k, n = C.c_int(0), C.c_int(0)
+        check("mpcqp_ctx_crash_params", lib().mpcqp_ctx_crash_params(self.ctx, C.byref(k),
+                                                                       C.byref(n)))
+        return (k.value, n.value)
+
+    @property
     def fused_kernel(self) -> str:
         """name of the kernel mpcqp_batch_solve launches: k_mpc_pair (two QPs per wave),
         k_mpc (one QP per wave) or the generic k_condense + k_solve pair"""

@@ -409,9 +409,141 @@ typedef struct {
     int *src;     /* m: original constraint id (see ordering above) */
 } gi_cons;
 
+/* Speculative primal-dual active-set start for problems whose constraints are all bounds (the
+ * GPU kernels' "crash").  From the unconstrained minimum x0 (H^-1 = J J'):
+ * the working set A starts as every violated bound (at most kmax: the ones already active, then
+ * the lowest variable ids); the minimiser with A's bounds as equalities is
+ *   x = x0 - J J_A' w,   M w = x0_A - b_A,   M = J_A J_A' = (H^-1)_AA,
+ * M solved by Gauss-Jordan without pivoting (M is positive definite), multipliers
+ * lambda_a = -side_a w_a, f = f0 + w'(x0_A - b_A) / 2.  The next working set drops the
+ * negative multipliers and adds the bounds x violates (GI_FEAS_TOL, as the dual loop's test);
+ * an unchanged set is the optimum of the strictly convex QP (KKT within the tolerance), the
+ * same point the dual active-set loop reaches.  Gives up (returns 0, x / fval untouched) after
+ * pmax working sets or a non-positive pivot: the caller then runs Goldfarb-Idnani from x0.
+ * *solves counts the working sets that needed a solve (the reported iterations). */
+static int box_crash(int n, const double *J, const double *x0, double fval0, const gi_cons *C,
+                     int kmax, int pmax, double *x, double *fval, double *u_cons, int *solves) {
+    int *lo_c = malloc(sizeof(int) * 2 * n), *up_c = lo_c + n;
+    int *side = calloc((size_t)2 * n, sizeof(int)), *nw = side + n;
+    int *A = malloc(sizeof(int) * (n + 1));
+    double *lam = calloc((size_t)n, sizeof(double)), *xc = malloc(sizeof(double) * n);
+    double *M = malloc(sizeof(double) * (size_t)n * n), *r = malloc(sizeof(double) * 3 * n);
+    double *r0 = r + n, *y = r + 2 * n;
+    double fv = fval0;
+    int ok = 0, it = 0, ns = 0;
+    for (int j = 0; j < n; ++j) { lo_c[j] = up_c[j] = -1; xc[j] = x0[j]; }
+    for (int c = 0; c < C->m; ++c) {
+        const int s = C->src[c];
+        if (C->is_eq[c] || s >= 2 * n) goto out; /* not a bounds-only problem */
+        if (s < n) lo_c[s] = c; else up_c[s - n] = c;
+    }
+    for (;;) {
+        int changed = 0, cnt = 0;
+        for (int j = 0; j < n; ++j) {
+            nw[j] = side[j];
+            if (side[j] == 0) {
+                if (lo_c[j] >= 0) {
+                    const double b = C->b[lo_c[j]];
+                    if (xc[j] - b < -GI_FEAS_TOL * (1.0 + fabs(b))) nw[j] = 1;
+                }
+                if (nw[j] == 0 && up_c[j] >= 0) {
+                    const double b = C->b[up_c[j]]; /* -ub */
+                    if (-xc[j] - b < -GI_FEAS_TOL * (1.0 + fabs(b))) nw[j] = -1;
+                }
+            } else if (lam[j] < 0.0) {
+                nw[j] = 0;
+            }
+            changed |= nw[j] != side[j];
+            cnt += nw[j] != 0;
+        }
+        if (!changed) { ok = 1; break; } /* (it = 0: x0 violates nothing) */
+        if (it >= pmax) break;
+        if (cnt > kmax) { /* kept bounds first, then new ones by variable id */
+            int kept = 0;
+            for (int j = 0; j < n; ++j) kept += side[j] != 0 && nw[j] != 0;
+            int room = kmax - kept;
+            for (int j = 0; j < n; ++j)
+                if (side[j] == 0 && nw[j] != 0) {
+                    if (room > 0) --room;
+                    else nw[j] = 0;
+                }
+        }
+        int k = 0;
+        for (int j = 0; j < n; ++j) {
+            side[j] = nw[j];
+            if (side[j]) A[k++] = j;
+        }
+        ++it;
+        if (k == 0) {
+            for (int j = 0; j < n; ++j) { xc[j] = x0[j]; lam[j] = 0.0; }
+            fv = fval0;
+            continue;
+        }
+        ++ns;
+        for (int i = 0; i < k; ++i) {
+            for (int m = 0; m < k; ++m) {
+                double s = 0.0;
+                for (int c = 0; c < n; ++c) s += J[IDX(A[i], c, n)] * J[IDX(A[m], c, n)];
+                M[IDX(i, m, k)] = s;
+            }
+            const int a = A[i];
+            const double b = side[a] > 0 ? C->b[lo_c[a]] : -C->b[up_c[a]];
+            r[i] = r0[i] = x0[a] - b;
+        }
+        int pd = 1;
+        for (int j = 0; j < k && pd; ++j) {
+            const double d = M[IDX(j, j, k)];
+            if (!(d > 0.0)) { pd = 0; break; }
+            const double inv = 1.0 / d;
+            for (int i = 0; i < k; ++i) {
+                if (i == j) continue;
+                const double l = M[IDX(i, j, k)] * inv;
+                for (int m = j + 1; m < k; ++m) M[IDX(i, m, k)] -= l * M[IDX(j, m, k)];
+                r[i] -= l * r[j];
+            }
+        }
+        if (!pd) break;
+        double wr = 0.0;
+        for (int i = 0; i < k; ++i) {
+            r[i] = r[i] / M[IDX(i, i, k)]; /* w */
+            wr += r[i] * r0[i];
+        }
+        for (int c = 0; c < n; ++c) {
+            double s = 0.0;
+            for (int i = 0; i < k; ++i) s += J[IDX(A[i], c, n)] * r[i];
+            y[c] = s;
+        }
+        for (int j = 0; j < n; ++j) {
+            double s = 0.0;
+            for (int c = 0; c < n; ++c) s += J[IDX(j, c, n)] * y[c];
+            xc[j] = x0[j] - s;
+            lam[j] = 0.0;
+        }
+        for (int i = 0; i < k; ++i) {
+            const int a = A[i];
+            xc[a] = side[a] > 0 ? C->b[lo_c[a]] : -C->b[up_c[a]];
+            lam[a] = -(double)side[a] * r[i];
+        }
+        fv = fval0 + 0.5 * wr;
+    }
+    if (ok) {
+        for (int j = 0; j < n; ++j) x[j] = xc[j];
+        *fval = fv;
+        if (u_cons) {
+            for (int c = 0; c < C->m; ++c) u_cons[c] = 0.0;
+            for (int j = 0; j < n; ++j)
+                if (side[j]) u_cons[side[j] > 0 ? lo_c[j] : up_c[j]] = lam[j];
+        }
+    }
+out:
+    *solves = ns;
+    free(lo_c); free(side); free(A); free(lam); free(xc); free(M); free(r);
+    return ok;
+}
+
 static int gi_solve(int n, double *Hf /* n x n, destroyed */, const double *g, gi_cons *C,
                     int max_iter, double *x, double *fval_out, int *iters_out,
-                    double *u_out /* m */) {
+                    double *u_out /* m */, int crash_kmax, int crash_pmax) {
     const int m = C->m;
     double *J = calloc((size_t)n * n, sizeof(double));
     double *Rm = calloc((size_t)n * n, sizeof(double));
@@ -460,6 +592,18 @@ static int gi_solve(int n, double *Hf /* n x n, destroyed */, const double *g, g
         x[i] = -s;
     }
     for (int i = 0; i < n; ++i) fval += 0.5 * g[i] * x[i];
+
+    if (crash_kmax > 0 && m > 0) {
+        int solves = 0;
+        if (box_crash(n, J, x, fval, C, crash_kmax, crash_pmax, x, &fval, u_out, &solves)) {
+            *fval_out = fval;
+            *iters_out = solves;
+            free(J); free(Rm); free(d); free(z); free(r); free(u); free(w); free(act);
+            free(isact);
+            return ORC_OK;
+        }
+        iters = solves; /* gave up: Goldfarb-Idnani from the unconstrained minimum */
+    }
 
     /* equality constraints first (full steps, never dropped), then the dual loop */
     int eq_next = 0;
@@ -612,10 +756,25 @@ done:
     return status;
 }
 
+static int solve_qp_impl(int n, const double *H, const double *f, int mA, const double *A,
+                         int a_colmajor, const double *lb, const double *ub, const double *lbA,
+                         const double *ubA, const orc_friction *fric, int max_iter, double *x,
+                         double *cost, int *iters, double *lam_bounds, double *lam_rows,
+                         int crash_kmax, int crash_pmax);
+
 int orc_solve_qp(int n, const double *H, const double *f, int mA, const double *A,
                  int a_colmajor, const double *lb, const double *ub, const double *lbA,
                  const double *ubA, const orc_friction *fric, int max_iter, double *x,
                  double *cost, int *iters, double *lam_bounds, double *lam_rows) {
+    return solve_qp_impl(n, H, f, mA, A, a_colmajor, lb, ub, lbA, ubA, fric, max_iter, x, cost,
+                         iters, lam_bounds, lam_rows, 0, 0);
+}
+
+static int solve_qp_impl(int n, const double *H, const double *f, int mA, const double *A,
+                         int a_colmajor, const double *lb, const double *ub, const double *lbA,
+                         const double *ubA, const orc_friction *fric, int max_iter, double *x,
+                         double *cost, int *iters, double *lam_bounds, double *lam_rows,
+                         int crash_kmax, int crash_pmax) {
     if (n <= 0 || mA < 0) return ORC_BAD_DIMS;
     int *pos = malloc(sizeof(int) * n);
     int *fid = malloc(sizeof(int) * n);
@@ -724,7 +883,7 @@ int orc_solve_qp(int n, const double *H, const double *f, int mA, const double *
     int it = 0;
     if (status == ORC_OK && nf > 0)
         status = gi_solve(nf, Hf, g, &C, max_iter > 0 ? max_iter : 10 * (C.m + nf + 1), xf,
-                          &fv, &it, uc);
+                          &fv, &it, uc, crash_kmax, crash_pmax);
     for (int i = 0; i < n; ++i) x[i] = pos[i] < 0 ? xB[i] : xf[pos[i]];
     if (cost) *cost = fv + c0;
     if (iters) *iters = it;
@@ -883,8 +1042,8 @@ static int srbm_one(const orc_srbm_cfg *cfg, const double *x0, const double *xre
                  NULL, NULL, NULL, NULL, NULL, NULL, NULL);
     orc_srbm_bounds(cfg, contact, lb, ub);
     orc_friction fr = {cfg->friction && cfg->model == 0, nu, N, 2, cfg->mu, contact};
-    int st = orc_solve_qp(nV, H, f, 0, NULL, 0, lb, ub, NULL, NULL, &fr, cfg->max_iter, U,
-                          cost, iters, NULL, NULL);
+    int st = solve_qp_impl(nV, H, f, 0, NULL, 0, lb, ub, NULL, NULL, &fr, cfg->max_iter, U,
+                           cost, iters, NULL, NULL, cfg->crash_kmax, cfg->crash_pmax);
     if (!Hout) free(H);
     if (!fout) free(f);
     free(lb);

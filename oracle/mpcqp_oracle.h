@@ -109,6 +109,10 @@ typedef struct {
     double u_min, u_max;    /* literal model input box */
     const double *Q, *R, *P;/* nx*nx, nu*nu, nx*nx col-major */
     int max_iter;
+    /* bounds-only problems: the GPU kernels' speculative primal-dual active-set start (at most
+     * crash_kmax bounds per working set, crash_pmax working sets, then Goldfarb-Idnani);
+     * 0 = off (plain Goldfarb-Idnani, the solve every other path runs) */
+    int crash_kmax, crash_pmax;
 } orc_srbm_cfg;
 
 /* x0: [B][nx]; xref: [B][N+1][nx]; lin: [B][8]; contact: [B]; U: [B][nu*N] */

@@ -34,7 +34,8 @@ class SrbmCfg(C.Structure):
                 ("mu", C.c_double), ("Ib", C.c_double * 9), ("fz_min", C.c_double),
                 ("fz_max", C.c_double), ("fxy_max", C.c_double), ("u_min", C.c_double),
                 ("u_max", C.c_double), ("Q", C.c_void_p), ("R", C.c_void_p),
-                ("P", C.c_void_p), ("max_iter", C.c_int)]
+                ("P", C.c_void_p), ("max_iter", C.c_int), ("crash_kmax", C.c_int),
+                ("crash_pmax", C.c_int)]
 
 
 def build() -> str:
@@ -198,6 +199,7 @@ def make_cfg(p):
     keep = [_f(p["Q"]), _f(p["R"]), _f(p["P"])]
     cfg.Q, cfg.R, cfg.P = [k.ctypes.data for k in keep]
     cfg.max_iter = p.get("max_iter", 0)
+    cfg.crash_kmax, cfg.crash_pmax = p.get("crash", (0, 0))
     return cfg, keep
 
 

@@ -165,8 +165,16 @@ def run_batch(p, batch, want_hf=False, expect_fast=True):
     eng.sync()
     for k in ("U", "cost", "status", "iters"):
         out[k] = d[k].cpu().numpy()
+    out["crash"] = eng.crash  # the oracle reproduces the iteration counts with p["crash"] = this
     eng.close()
     return out
+
+
+def with_crash(p, crash):
+    """the oracle configured with the library kernel's crash start (iteration counts)"""
+    q = dict(p)
+    q["crash"] = tuple(crash)
+    return q
 
 
 @pytest.mark.parametrize("fname", ["srbm_B.npz", "srbm_C.npz", "literal_L.npz"])
@@ -193,8 +201,9 @@ def test_batch_vs_oracle(gpu, orc, config, B):
     p = mpcqp.model_params(config)
     batch = mpcqp.make_batch(p, B, seed=99)
     o = run_batch(p, batch, want_hf=True)
-    ref = orc.srbm_batch(p, batch["x0"], batch["xref"], batch["lin"], batch["contact"],
-                         want_hf=True)
+    ref = orc.srbm_batch(with_crash(p, o["crash"]), batch["x0"], batch["xref"], batch["lin"],
+                         batch["contact"], want_hf=True)
+    assert (o["crash"][0] > 0) == (config == "B")  # the paired kernel's crash start
     np.testing.assert_array_equal(o["status"], ref["status"])
     np.testing.assert_array_equal(o["gen_status"], ref["status"])
     assert np.all(o["status"] == 0)
@@ -206,7 +215,8 @@ def test_batch_vs_oracle(gpu, orc, config, B):
     bad = [i for i in range(B) if not u_close(o["U"][i], ref["U"][i])]
     assert not bad, bad[:10]
     np.testing.assert_allclose(o["cost"], ref["cost"], rtol=1e-9, atol=1e-9)
-    # same algorithm, same order: iteration counts agree except on rounding-level ties
+    # same algorithm, same order: iteration counts agree except on rounding-level ties (the
+    # paired kernel's crash start included: the oracle runs it with the same caps)
     assert np.mean(o["iters"] == ref["iters"]) >= 0.99
 
 
@@ -414,18 +424,24 @@ def test_pair_kernel_matches_single_and_oracle(gpu, orc, monkeypatch):
     assert bad_dims.sum() > 20 and (nfree < 30).sum() > 20
     np.testing.assert_array_equal(pair["status"], single["status"])
     assert np.all(pair["status"][bad_dims] == 1) and np.all(pair["status"][~bad_dims] == 0)
-    np.testing.assert_array_equal(pair["iters"], single["iters"])
+    # iteration counts: the one-QP kernel runs the plain dual loop, the paired kernel its crash
+    # start first -- each against the oracle configured the same way (below)
+    assert single["crash"] == (0, 0) and pair["crash"][0] > 0
     # blocked MFMA factorisation in the one-QP kernel vs column sweeps in the paired one
     sc = np.maximum(1.0, np.abs(single["U"]).max(axis=1, keepdims=True))
     assert np.all(np.abs(pair["U"] - single["U"]) <= 1e-10 * sc)
     np.testing.assert_allclose(pair["cost"], single["cost"], rtol=1e-10, atol=1e-10)
     ok = ~bad_dims
     ref = orc.srbm_batch(p, batch["x0"][ok], batch["xref"][ok], batch["lin"][ok], ct[ok])
-    assert np.all(ref["status"] == 0)
+    refc = orc.srbm_batch(with_crash(p, pair["crash"]), batch["x0"][ok], batch["xref"][ok],
+                          batch["lin"][ok], ct[ok])
+    assert np.all(ref["status"] == 0) and np.all(refc["status"] == 0)
     Uo = pair["U"][ok]
     bad = [j for j in range(Uo.shape[0]) if not u_close(Uo[j], ref["U"][j])]
     assert not bad, bad[:10]
     np.testing.assert_allclose(pair["cost"][ok], ref["cost"], rtol=1e-9, atol=1e-9)
+    assert np.mean(single["iters"][ok] == ref["iters"]) >= 0.99
+    assert np.mean(pair["iters"][ok] == refc["iters"]) >= 0.99
     assert len(set(pair["iters"][ok].tolist())) > 2  # uneven work inside the waves
 
 
@@ -462,7 +478,9 @@ def test_pair_kernel_full_size_vs_single(gpu, monkeypatch):
     a, b = res[True], res[False]
     assert np.all(a["status"] == 0) and np.all(b["status"] == 0)
     assert np.all(np.isfinite(a["U"])) and np.all(np.isfinite(a["cost"]))
-    np.testing.assert_array_equal(a["iters"], b["iters"])
+    # the crash start solves the same QPs in fewer passes: the tail above all
+    assert a["iters"].mean() < 0.6 * b["iters"].mean()
+    assert a["iters"].max() <= 10 < b["iters"].max()
     scale = np.maximum(1.0, np.abs(b["U"]).max(axis=1, keepdims=True))
     assert np.all(np.abs(a["U"] - b["U"]) <= 1e-10 * scale)
     np.testing.assert_allclose(a["cost"], b["cost"], rtol=1e-10, atol=1e-10)
@@ -479,12 +497,15 @@ def test_pair_kernel_literal_model(gpu, orc, monkeypatch):
     monkeypatch.delenv("MPCQP_PAIR")
     pair = run_batch(p, batch)
     np.testing.assert_array_equal(pair["status"], single["status"])
-    np.testing.assert_array_equal(pair["iters"], single["iters"])
     sc = np.maximum(1.0, np.abs(single["U"]).max(axis=1, keepdims=True))
     assert np.all(np.abs(pair["U"] - single["U"]) <= 1e-10 * sc)
     ref = orc.srbm_batch(p, batch["x0"], batch["xref"], batch["lin"], batch["contact"])
+    refc = orc.srbm_batch(with_crash(p, pair["crash"]), batch["x0"], batch["xref"], batch["lin"],
+                          batch["contact"])
     for i in range(B):
         assert u_close(pair["U"][i], ref["U"][i]), i
+    assert np.mean(single["iters"] == ref["iters"]) >= 0.99
+    assert np.mean(pair["iters"] == refc["iters"]) >= 0.99
 
 
 def test_friction_rows_mixed_contact_vs_oracle(gpu, orc):
@@ -780,3 +801,31 @@ def test_solve_select_fused_record(gpu, config, gait, B, max_free):
         eng.sync()
         np.testing.assert_array_equal(got, rec2.cpu().numpy())
     eng.close()
+
+
+@pytest.mark.parametrize("crash_p", ["0", "1", "2"])
+def test_pair_crash_fallback_paths(gpu, orc, monkeypatch, crash_p):
+    """the paired kernel's crash start capped at 0 / 1 / 2 working sets (MPCQP_CRASH_P): 0 is
+    the plain dual loop (iteration counts equal the one-QP kernel's), 1 and 2 give up on most
+    constrained instances and fall back to the dual loop from the unconstrained minimum (counts
+    = working sets tried + dual passes).  U / cost equal the oracle's optimum everywhere, the
+    iteration counts the oracle's run with the same caps."""
+    import mpcqp
+    p = mpcqp.model_params("B")
+    B = 1024
+    batch = mpcqp.make_batch(p, B, seed=41)
+    monkeypatch.setenv("MPCQP_CRASH_P", crash_p)
+    o = run_batch(p, batch)
+    assert o["crash"][1] == int(crash_p)
+    ref = orc.srbm_batch(with_crash(p, o["crash"]), batch["x0"], batch["xref"], batch["lin"],
+                         batch["contact"])
+    assert np.all(o["status"] == 0) and np.all(ref["status"] == 0)
+    bad = [i for i in range(B) if not u_close(o["U"][i], ref["U"][i])]
+    assert not bad, bad[:10]
+    np.testing.assert_allclose(o["cost"], ref["cost"], rtol=1e-9, atol=1e-9)
+    assert np.mean(o["iters"] == ref["iters"]) >= 0.99
+    if crash_p == "0":
+        plain = orc.srbm_batch(p, batch["x0"], batch["xref"], batch["lin"], batch["contact"])
+        assert np.mean(o["iters"] == plain["iters"]) >= 0.99
+    else:  # some instances fell back: more iterations than working sets
+        assert (o["iters"] > int(crash_p)).any()
