@@ -46,6 +46,11 @@ struct MpcArgs {
     double fz_min, fz_max, fxy_max, u_min, u_max, mu;
     int max_iter, max_free;
     int crash_p;  // paired kernel: working sets of its crash start before the dual loop (0: none)
+    // paired kernel's bound constants, by kind of free variable (v: a vertical force, t: a
+    // tangential force; the literal model's inputs use v): b of x >= lo (lo) and of -x >= -hi
+    // (-hi), and the dual loop's violation thresholds -kFeasTol (1 + |b|), precomputed on the
+    // host so the kernel selects them from scalar registers instead of keeping them per lane
+    double blo_v, blo_t, bhi_v, bhi_t, tlo_v, tlo_t, thi_v, thi_t;
     const double *lin, *x0, *xref;
     const uint64_t *contact;
     double *U, *cost;

@@ -64,7 +64,7 @@ namespace mpcqp {
 constexpr int kPairNF = 30;  // free variables per instance; lane 31 of a half carries g
 // crash start (below): bounds per working set, working sets before giving up
 #ifndef MPCQP_CRASH_K
-#define MPCQP_CRASH_K 15
+#define MPCQP_CRASH_K 12
 #endif
 #ifndef MPCQP_CRASH_P
 #define MPCQP_CRASH_P 8
@@ -693,10 +693,18 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             stb = (lo > -kInfty ? 1 : 0) | (hi < kInfty ? 2 : 0) |
                   ((MODEL == 0 && (fid[hl] % NU) % 3 == 2) ? 4 : 0);
         }
-        auto blo_of = [&](int sb) { return MODEL == 1 ? a.u_min : ((sb & 4) ? a.fz_min : -a.fxy_max); };
-        auto bhi_of = [&](int sb) { return MODEL == 1 ? -a.u_max : ((sb & 4) ? -a.fz_max : -a.fxy_max); };
-        const double blo = blo_of(stb), bhi = bhi_of(stb);  // (bit 2 of stb never changes)
-        const double tlo = -kFeasTol * (1.0 + fabs(blo)), thi = -kFeasTol * (1.0 + fabs(bhi));
+        // b and the violation threshold of the lane's two bounds: host-computed constants picked
+        // by bit 2 of stb (which never changes) at each use -- the opaque copy of the bit keeps
+        // the selects where they are used, so no per-lane copy lives through the loops
+        auto vert = [&]() {
+            int sb = stb;
+            asm volatile("" : "+v"(sb));
+            return (sb & 4) != 0;
+        };
+#define MPCQP_BLO (vert() ? a.blo_v : a.blo_t)
+#define MPCQP_BHI (vert() ? a.bhi_v : a.bhi_t)
+#define MPCQP_TLO (vert() ? a.tlo_v : a.tlo_t)
+#define MPCQP_THI (vert() ? a.thi_v : a.thi_t)
         bool done = !ok2;
 #if MPCQP_PAIR_CRASH
         // ---- crash: speculative primal-dual active-set start (oracle box_crash, DESIGN.md
@@ -712,8 +720,12 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         //      or a non-positive pivot the half gives up with J, x0 and f0 untouched and runs
         //      Goldfarb-Idnani as before.  Iterations = the working sets that needed a solve.
         //      One wavefront loop for both halves; every ballot runs with all lanes active.
+        //      Rows of M and the terms of y go in chunks of four (one branch per chunk, the
+        //      chunk's LDS reads issued together); past-k entries of a chunk are computed from
+        //      clamped addresses and never read.
         {
-            constexpr int KC = kPairCrashK;
+            constexpr int KC = kPairCrashK, CH = 4;
+            static_assert(KC % CH == 0, "whole chunks");
             const int PC = a.crash_p;
             static_assert(KC * NF <= Lay::NR, "the published J rows fit the dead L space");
             static_assert(KC + 2 <= NP, "the pivot row fits the row buffer");
@@ -728,9 +740,11 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             while (__ballot(crashing) != 0ull) {
                 int nw = side;
                 if (crashing && hl < nf) {
+                    // (the thresholds are re-derived here: kept live across the loop they were
+                    //  the kernel's spilled registers, reloaded from scratch every trip)
                     if (side == 0) {
-                        if ((stb & 1) && xc - blo < tlo) nw = 1;
-                        else if ((stb & 2) && -xc - bhi < thi) nw = -1;
+                        if ((stb & 1) && xc - MPCQP_BLO < MPCQP_TLO) nw = 1;
+                        else if ((stb & 2) && -xc - MPCQP_BHI < MPCQP_THI) nw = -1;
                     } else if (lam < 0.0) {
                         nw = 0;
                     }
@@ -758,7 +772,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 const int ks = solving ? k : 0;
                 const int kmax = max(__builtin_amdgcn_readlane(ks, 0), __builtin_amdgcn_readlane(ks, kHalf));
                 if (kmax == 0) continue;  // (wave-uniform)
-                const double bval = side > 0 ? blo : -bhi;
+                const double bval = side > 0 ? MPCQP_BLO : -MPCQP_BHI;
                 const double r0 = x0v - bval;
                 double rr = r0;
                 if (inA) {
@@ -769,17 +783,22 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 // row rank(a) of M = J_A J_A' (lane a's own J row against the published rows)
                 double Mr[KC];
         #pragma unroll
-                for (int m = 0; m < KC; ++m) {
-                    Mr[m] = 0.0;
-                    if (m < kmax) {
-                        double s4[4] = {0.0, 0.0, 0.0, 0.0};
+                for (int m0 = 0; m0 < KC; m0 += CH) {
         #pragma unroll
-                        for (int c = 0; c < NF; ++c) s4[c & 3] += Jr[c] * Wr[m * NF + c];
-                        Mr[m] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+                    for (int m = m0; m < m0 + CH; ++m) Mr[m] = 0.0;
+                    if (m0 < kmax) {
+        #pragma unroll
+                        for (int c = 0; c < NF; ++c) {
+        #pragma unroll
+                            for (int m = 0; m < CH; ++m) Mr[m0 + m] += Jr[c] * Wr[(m0 + m) * NF + c];
+                            if ((c % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
+                        }
                     }
                 }
                 // Gauss-Jordan without pivoting (M is positive definite): step j's pivot row is
-                // published by the lane of rank j, every other lane of A eliminates column j
+                // published by the lane of rank j, every other lane of A eliminates column j.
+                // (The next pivot's stores follow this step's loads of the same words, and LDS
+                //  keeps a wave's program order: one wave_sync per step.)
                 double dd = 1.0;
                 bool bad = false;
         #pragma unroll
@@ -794,13 +813,15 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                             bad |= !(Mr[j] > 0.0);
                         }
                         wave_sync();
-                        if (inA && rho != j && j < k) {
-                            const double l = Mr[j] * Pv[KC + 1];
+                        double pv[KC + 2];
         #pragma unroll
-                            for (int m = j + 1; m < KC; ++m) Mr[m] -= l * Pv[m];
-                            rr -= l * Pv[KC];
+                        for (int m = j + 1; m < KC + 2; ++m) pv[m] = Pv[m];
+                        if (inA && rho != j && j < k) {
+                            const double l = Mr[j] * pv[KC + 1];
+        #pragma unroll
+                            for (int m = j + 1; m < KC; ++m) Mr[m] -= l * pv[m];
+                            rr -= l * pv[KC];
                         }
-                        wave_sync();
                     }
                 }
                 const bool gave_up = half_ballot(bad) != 0u;
@@ -808,9 +829,19 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 if (inA) Wv[rho] = w;
                 wave_sync();
                 // y = J_A' w (lane c: column c of the published rows), then x = x0 - J y
-                double y = 0.0;
-                for (int m = 0; m < kmax; ++m) y += (m < k ? Wr[m * NF + (hl < NF ? hl : 0)] * Wv[m] : 0.0);
-                if (hl < NF) Yv[hl] = y;
+                double yv[CH] = {0.0, 0.0, 0.0, 0.0};
+                const int cc = hl < NF ? hl : 0;
+        #pragma unroll
+                for (int m0 = 0; m0 < KC; m0 += CH) {
+                    if (m0 < kmax) {
+        #pragma unroll
+                        for (int m = 0; m < CH; ++m) {
+                            const double t = Wr[(m0 + m) * NF + cc] * Wv[m0 + m];
+                            yv[m] += (m0 + m < k) ? t : 0.0;
+                        }
+                    }
+                }
+                if (hl < NF) Yv[hl] = (yv[0] + yv[1]) + (yv[2] + yv[3]);
                 wave_sync();
                 double s4[4] = {0.0, 0.0, 0.0, 0.0};
         #pragma unroll
@@ -865,7 +896,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                     for (int c = 0; c < NF; ++c) {
                         rowbuf[c] = Jr[c];
                     }
-                    rowbuf[NP - 1] = lower ? x - blo : -x - bhi;
+                    rowbuf[NP - 1] = lower ? x - MPCQP_BLO : -x - MPCQP_BHI;
                 }
                 wave_sync();
                 dj = (hl < nf) ? sg * rowbuf[hl] : 0.0;
@@ -1072,12 +1103,12 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 double best = INFINITY;
                 bool upb = false;  // the lane's candidate is its upper bound (id hl + nf)
                 if (stb & 1) {
-                    const double s_ = x - blo;
-                    if (s_ < tlo) best = s_;
+                    const double s_ = x - MPCQP_BLO;
+                    if (s_ < MPCQP_TLO) best = s_;
                 }
                 if (stb & 2) {
-                    const double s_ = -x - bhi;
-                    if ((s_ < thi) & (s_ < best)) { best = s_; upb = true; }
+                    const double s_ = -x - MPCQP_BHI;
+                    if ((s_ < MPCQP_THI) & (s_ < best)) { best = s_; upb = true; }
                 }
                 // lowest id among the lanes at the minimum: a lower bound (id hl) before any upper
                 // bound (hl + nf), each by lowest lane
@@ -1140,6 +1171,10 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     #endif
     }
 
+#undef MPCQP_BLO
+#undef MPCQP_BHI
+#undef MPCQP_TLO
+#undef MPCQP_THI
     MPCQP_STAMP(a.stamps, 8, tst);
     MPCQP_CUT(a.cut, 7);
     // ---- outputs.  The lane-derived values (half lane, this half's LDS base and its free map)

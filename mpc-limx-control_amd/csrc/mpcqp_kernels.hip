@@ -1186,6 +1186,17 @@ static MpcArgs mpc_args(mpcqp_ctx *c, int B) {
     a.max_iter = m.max_iter;
     a.max_free = m.max_free > 0 ? m.max_free : m.nu * m.N;
     a.crash_p = c->fk.crash_p;
+    {   // (pair_mpc's bound selection; gi_solver.hpp kFeasTol)
+        const bool lit = m.model == MPCQP_MODEL_LITERAL;
+        a.blo_v = lit ? m.u_min : m.fz_min;
+        a.blo_t = lit ? m.u_min : -m.fxy_max;
+        a.bhi_v = lit ? -m.u_max : -m.fz_max;
+        a.bhi_t = lit ? -m.u_max : -m.fxy_max;
+        a.tlo_v = -kFeasTol * (1.0 + fabs(a.blo_v));
+        a.tlo_t = -kFeasTol * (1.0 + fabs(a.blo_t));
+        a.thi_v = -kFeasTol * (1.0 + fabs(a.bhi_v));
+        a.thi_t = -kFeasTol * (1.0 + fabs(a.bhi_t));
+    }
     a.stamps = c->dstamps;
     a.cut = 0;
 #ifdef MPCQP_CUTS

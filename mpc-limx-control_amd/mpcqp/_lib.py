@@ -79,8 +79,9 @@ def lib():
     L.mpcqp_batch_solve_qp.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp]
     L.mpcqp_batch_solve.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp]
     L.mpcqp_ctx_fast_path.argtypes = [vp]
-    L.mpcqp_ctx_one_wave_nf.argtypes = [vp]
-    L.mpcqp_ctx_crash_params.argtypes = [vp, vp, vp]
+    for name, at in (("mpcqp_ctx_one_wave_nf", [vp]), ("mpcqp_ctx_crash_params", [vp, vp, vp])):
+        if hasattr(L, name):  # absent from A/B builds of older sources
+            getattr(L, name).argtypes = at
     L.mpcqp_debug_phase_cycles.argtypes = [vp, vp, i]
     L.mpcqp_batch_solve_host.argtypes = [vp, i] + [vp] * 8
     L.mpcqp_batch_discretize.argtypes = [vp, i, vp, vp]

@@ -104,6 +104,8 @@ class BatchEngine:
         """(bounds per working set, working sets) of the one-wave kernel's crash start, (0, 0)
         if none: the oracle reproduces its iteration counts with p["crash"] set to this"""
         import ctypes as C
+        if not hasattr(lib(), "mpcqp_ctx_crash_params"):  # an A/B build of older sources
+            return (0, 0)
         k, n = C.c_int(0), C.c_int(0)
         check("mpcqp_ctx_crash_params", lib().mpcqp_ctx_crash_params(self.ctx, C.byref(k),
                                                                        C.byref(n)))
