@@ -20,7 +20,7 @@ __global__ void __launch_bounds__(WgShape<NU * N>::THREADS, MPCQP_DENSE_W) k_den
     extern __shared__ __attribute__((aligned(16))) unsigned char smem_d[];
     // one workgroup per QP (grid = B): no grid-stride loop, so nothing is hoisted out of a loop
     // and kept live across the whole body
-    const int b = blockIdx.x;
+    const int b = xcd_order((int)blockIdx.x, (int)gridDim.x);
     if (b < a.B) dense_mpc_one<NX, NU, N, TOEP>(a, b, smem_d);
 }
 

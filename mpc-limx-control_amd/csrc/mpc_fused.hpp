@@ -517,7 +517,7 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     static_assert(!GEN || MODEL == 0, "generated inputs are defined for the SRBM model");
     using Lay = MpcLayout<NU, N, FRIC, NF>;
     constexpr int NX = 13, NS = NX + NU, NV = Lay::NV, LD = Lay::LD;
-    const int b = blockIdx.x, ln = lane();
+    const int b = xcd_order((int)blockIdx.x, (int)gridDim.x), ln = lane();
     double *D = reinterpret_cast<double *>(smem);
     double *X0 = D + Lay::oX0, *X1 = D + Lay::oX1, *S = D + Lay::oS, *UV = D + Lay::oUV;
     static_assert(MODEL == 0 || MODEL == 1, "TRON1 models only");

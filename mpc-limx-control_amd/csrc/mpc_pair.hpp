@@ -153,7 +153,8 @@ __device__ __forceinline__ int row_bcast_u32(int v, int j) {
 template <bool GEN>
 __device__ __forceinline__ int pair_sorted_instance(const MpcArgs &a) {
     const int ln = lane(), c = ln & 15;
-    const int g0 = (2 * (int)blockIdx.x) & ~15;
+    const int wv = xcd_order((int)blockIdx.x, (int)gridDim.x);
+    const int g0 = (2 * wv) & ~15;
     const int gn = a.B - g0 < 16 ? a.B - g0 : 16;
     unsigned long long key = ~0ull;
     if (c < gn) {
@@ -174,7 +175,7 @@ __device__ __forceinline__ int pair_sorted_instance(const MpcArgs &a) {
         rank += (j < gn && (kj < key || (kj == key && j < c))) ? 1 : 0;
     }
     // ranks 2w' (lower half) and 2w'+1 (upper half), both read off lanes 0-15 (row 0)
-    const int r0 = (2 * (int)blockIdx.x) & 15;
+    const int r0 = (2 * wv) & 15;
     const unsigned m0 = (unsigned)(__ballot(ln < 16 && c < gn && rank == r0) & 0xffffull);
     const unsigned m1 = (unsigned)(__ballot(ln < 16 && c < gn && rank == r0 + 1) & 0xffffull);
     const unsigned m = ln >= kHalf ? m1 : m0;
@@ -191,7 +192,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     MPCQP_STAMP_INIT(tst);
     const int ln = lane(), hl = ln & (kHalf - 1);
     const bool up = ln >= kHalf;
-    int bq = 2 * (int)blockIdx.x + (up ? 1 : 0);
+    int bq = 2 * xcd_order((int)blockIdx.x, (int)gridDim.x) + (up ? 1 : 0);
     if constexpr (MPCQP_PAIR_SORT && MODEL == 0) bq = pair_sorted_instance<GEN>(a);
     const bool valid = bq < a.B;
     const int b = valid ? bq : a.B - 1;  // the spare half of an odd batch re-reads the last QP
@@ -610,9 +611,12 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                     bad |= !(pivn > 0.0);
                     ikn = rsqrt_nr(pivn);
                 }
+                // the panel's CB columns of L go to a column buffer for the trailing update's
+                // broadcast reads: every lane stores its entry at a fixed slot (no predicate, no
+                // address arithmetic; entries above the diagonal are never read).  L itself is
+                // not kept: the fused sweep builds J as it goes, and the region is R^-1 next.
     #pragma unroll
-                for (int c = 0; c < CB; ++c)
-                    if (hl >= k + c && hl < NF) Lc[ccol(k + c, NF) + hl - k - c] = lk[c];
+                for (int c = 0; c < CB; ++c) Lc[c * NP + hl] = lk[c];
     #pragma unroll
                 for (int c = 0; c < CB; ++c) {
     #pragma unroll
@@ -625,7 +629,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                     if (j >= k + CB) {
                         double cv[CB];
     #pragma unroll
-                        for (int c = 0; c < CB; ++c) cv[c] = Lc[ccol(k + c, NF) + j - k - c];
+                        for (int c = 0; c < CB; ++c) cv[c] = Lc[c * NP + j];
     #pragma unroll
                         for (int c = 0; c < CB; ++c) h[j] -= lk[c] * cv[c];
     #pragma unroll
@@ -863,6 +867,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             }
         }
 #endif
+        MPCQP_CUT(a.cut, 8);
         bool fresh = true;
         int p = 0;
         // the partial multiplier of the constraint being added (slot q), in every lane of the half

@@ -13,6 +13,25 @@ constexpr int kWave = 64;
 
 __device__ __forceinline__ int lane() { return (int)__lane_id(); }
 
+// XCD-aware workgroup order (cdna_hip_programming.md T1, the bijective form): the dispatcher
+// deals workgroups round-robin over the 8 XCDs, so workgroups w and w + 1 sit on different
+// XCDs and every 128-B line shared by neighbouring instances (x0, lin, contact, the edges of
+// xref and U, cost / status / iterations) is fetched, and partially written, by several XCDs'
+// L2s.  Renumbered so that the workgroups of one XCD take one contiguous range of instances.
+// A speed choice only: any bijection is correct.
+#ifndef MPCQP_XCD_REMAP
+#define MPCQP_XCD_REMAP 1
+#endif
+__device__ __forceinline__ int xcd_order(int w, int G) {
+#if MPCQP_XCD_REMAP
+    const int q = G >> 3, r = G & 7, x = w & 7, s = w >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + s;
+#else
+    (void)G;
+    return w;
+#endif
+}
+
 // Broadcast lane `src` (wave-uniform index) of a double to the whole wave (v_readlane x2).
 __device__ __forceinline__ double readlane(double v, int src) {
     const long long b = __double_as_longlong(v);

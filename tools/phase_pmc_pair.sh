@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 export MPCQP_LIB="$(pwd)/mpc-limx-control_amd/lib/libmpcqp_cuts.so"
 R=$(pwd)
-CUTS="11 1 13 2 3 4 6 7 0"
+CUTS="11 1 13 2 3 4 6 8 7 0"
 for cut in $CUTS; do
   MPCQP_CUT=$cut timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
       SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 \
@@ -21,7 +21,8 @@ python3 - "$OUT/$CFG" "$CUTS" <<'PY'
 import csv, glob, sys, collections
 base, cuts = sys.argv[1], [int(c) for c in sys.argv[2].split()]
 names = {11: "inputs (+ pairing)", 1: "free map", 13: "model", 2: "S + u/v", 3: "g + H build + rows",
-         4: "Cholesky + inverse", 6: "unconstrained min", 7: "dual loop", 0: "outputs"}
+         4: "Cholesky + inverse", 6: "unconstrained min", 8: "crash start",
+         7: "dual loop", 0: "outputs"}
 K = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "F64")
 prev = None
 print(f"{'phase':22s} {'VALU/wave':>10s} {'F64/wave':>9s} {'SALU/wave':>10s} {'LDS/wave':>9s}")
