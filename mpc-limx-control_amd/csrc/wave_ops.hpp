@@ -229,13 +229,23 @@ __device__ __forceinline__ void pin(double &v) { asm volatile("" : "+v"(v)); }
 
 // Per-instance inputs and outputs are touched once: stream them past L2 (non-temporal) so they
 // do not evict the scratch lines of the waves' spilled registers, which otherwise leave L2 as
-// write-backs (MPCQP_STREAM=0: ordinary loads / stores)
+// write-backs (MPCQP_STREAM=0: ordinary loads; MPCQP_STREAM_LD / _ST pick each side)
 #ifndef MPCQP_STREAM
 #define MPCQP_STREAM 1
 #endif
+#ifndef MPCQP_STREAM_LD
+#define MPCQP_STREAM_LD MPCQP_STREAM
+#endif
+// Stores are ordinary (r04): with the XCD-aware instance order (xcd_order) neighbouring
+// instances' partial output lines meet in one XCD's L2 and leave it merged -- writes at config
+// B 47.3 -> 35.1 MB per launch (32.8 MB of U / cost / status / iterations), C 85.9 -> 66.1 MB
+// (64.0), time unchanged; non-temporal stores leave every partial line as its own HBM write
+#ifndef MPCQP_STREAM_ST
+#define MPCQP_STREAM_ST 0
+#endif
 template <typename T>
 __device__ __forceinline__ T stream_load(const T *p) {
-#if MPCQP_STREAM
+#if MPCQP_STREAM_LD
     return __builtin_nontemporal_load(p);
 #else
     return *p;
@@ -243,7 +253,7 @@ __device__ __forceinline__ T stream_load(const T *p) {
 }
 template <typename T>
 __device__ __forceinline__ void stream_store(T *p, T v) {
-#if MPCQP_STREAM
+#if MPCQP_STREAM_ST
     __builtin_nontemporal_store(v, p);
 #else
     *p = v;

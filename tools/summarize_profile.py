@@ -76,6 +76,9 @@ def main():
     ap.add_argument("--kernel", default="k_mpc_pair<6, 10, 0, false>")
     ap.add_argument("--grid", type=int, default=None,
                     help="threads per launch (default: 32 x batch, the pair kernel's grid)")
+    ap.add_argument("--no-traffic-json", action="store_true",
+                    help="per-config runs (C, E): do not overwrite profiles/pmc_traffic.json, the "
+                         "headline figure bench.py reads")
     a = ap.parse_args()
     out = os.path.join(ROOT, "profiles")
     stats = os.path.join(a.prof, "trace", "run_kernel_stats.csv")
@@ -100,7 +103,7 @@ def main():
                 write_samples=nw, hbm_bytes_per_launch=traffic,
                 correction="reads = 2 x FETCH_SIZE (gfx950 half-count), writes = WRITE_SIZE")
     json.dump(summ, open(os.path.join(out, f"{a.tag}_summary.json"), "w"), indent=1)
-    if traffic is not None:
+    if traffic is not None and not a.no_traffic_json:
         json.dump(dict(config=a.config, batch=a.batch, kernel=a.kernel, grid=grid, tag=a.tag,
                    lib_build_id=summ["lib_build_id"],
                    hbm_bytes_per_launch=traffic, read_bytes=2.0 * fetch * 1024 if fetch else None,

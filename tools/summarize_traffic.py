@@ -24,8 +24,11 @@ def main():
     ap.add_argument("--kernel", required=True)
     ap.add_argument("--grid", type=int, required=True)
     a = ap.parse_args()
-    fetch, nf = counter(os.path.join(a.dir, "FETCH_SIZE", "run_counter_collection.csv"), a.kernel, a.grid)
-    write, nw = counter(os.path.join(a.dir, "WRITE_SIZE", "run_counter_collection.csv"), a.kernel, a.grid)
+    sub = (lambda n, alt: n if os.path.isdir(os.path.join(a.dir, n)) else alt)
+    fetch, nf = counter(os.path.join(a.dir, sub("FETCH_SIZE", "fetch"), "run_counter_collection.csv"),
+                        a.kernel, a.grid)
+    write, nw = counter(os.path.join(a.dir, sub("WRITE_SIZE", "write"), "run_counter_collection.csv"),
+                        a.kernel, a.grid)
     if fetch is None or write is None:
         sys.exit(f"no launches of {a.kernel} at grid {a.grid} in {a.dir}")
     out = dict(config=a.config, batch=a.batch, kernel=a.kernel, grid=a.grid, tag=a.tag,
