@@ -1086,8 +1086,8 @@ static int dense_one(const orc_dense_cfg *cfg, const double *x0, const double *x
     orc_build_qp(nx, nu, N, Ad, Bd, cfg->Q, cfg->R, cfg->P, NULL, NULL, 0, 0, x0, xref, H, f,
                  NULL, NULL, NULL, NULL, NULL, NULL, NULL);
     for (int v = 0; v < nV; ++v) { lb[v] = cfg->u_min; ub[v] = cfg->u_max; }
-    int st = orc_solve_qp(nV, H, f, 0, NULL, 0, lb, ub, NULL, NULL, NULL, cfg->max_iter, U,
-                          cost, iters, NULL, NULL);
+    int st = solve_qp_impl(nV, H, f, 0, NULL, 0, lb, ub, NULL, NULL, NULL, cfg->max_iter, U,
+                           cost, iters, NULL, NULL, cfg->crash_kmax, cfg->crash_pmax);
     if (!Hout) free(H);
     if (!fout) free(f);
     free(lb);

@@ -141,6 +141,7 @@ typedef struct {
     const double *Q, *R, *P; /* nx*nx, nu*nu, nx*nx column-major (dense) */
     double u_min, u_max;
     int max_iter;
+    int crash_kmax, crash_pmax; /* as orc_srbm_cfg */
 } orc_dense_cfg;
 
 int orc_dense_batch(const orc_dense_cfg *cfg, int B, const double *x0, const double *xref,

@@ -47,7 +47,8 @@ def build() -> str:
 class DenseCfg(C.Structure):
     _fields_ = [("nx", C.c_int), ("nu", C.c_int), ("N", C.c_int), ("Ts", C.c_double),
                 ("Q", C.c_void_p), ("R", C.c_void_p), ("P", C.c_void_p), ("u_min", C.c_double),
-                ("u_max", C.c_double), ("max_iter", C.c_int)]
+                ("u_max", C.c_double), ("max_iter", C.c_int), ("crash_kmax", C.c_int),
+                ("crash_pmax", C.c_int)]
 
 
 def lib():
@@ -271,8 +272,9 @@ def dense_batch(p, x0, xref, AB, nthreads=0, want_hf=False):
     """config E (dense continuous model per instance): discretize -> literal dense condensing ->
     box-constrained Goldfarb-Idnani.  AB [B, nx*(nx+nu)] = [Ac | Bc] column-major."""
     keep = [_f(p["Q"]), _f(p["R"]), _f(p["P"])]
+    ck, cp = p.get("crash", (0, 0))
     cfg = DenseCfg(p["nx"], p["nu"], p["N"], p["Ts"], keep[0].ctypes.data, keep[1].ctypes.data,
-                   keep[2].ctypes.data, p["u_min"], p["u_max"], p.get("max_iter", 0))
+                   keep[2].ctypes.data, p["u_min"], p["u_max"], p.get("max_iter", 0), ck, cp)
     B = int(x0.shape[0])
     nV = p["nu"] * p["N"]
     U = np.zeros(B * nV)
