@@ -181,11 +181,13 @@ int mpcqp_ctx_fast_path(const mpcqp_ctx *ctx);
  * otherwise; 0 on the generic path): an instance with more goes to the overflow workgroup kernel
  * (bench.py counts the one-wave kernel's work over the instances it solved) */
 int mpcqp_ctx_one_wave_nf(const mpcqp_ctx *ctx);
-/* the crash start of the context's one-wave kernel (the paired kernel: a speculative
- * primal-dual active-set start before the dual loop): at most *kmax bounds
- * per working set, *pmax working sets before it falls back to the plain dual loop; 0 / 0 when
- * the context's kernels start the dual loop cold.  Reported iterations count its working sets. */
-int mpcqp_ctx_crash_params(const mpcqp_ctx *ctx, int *kmax, int *pmax);
+/* the crash start of the context's kernels (a speculative primal-dual active-set start before the
+ * dual loop): at most *kmax bounds per working set, *pmax working sets
+ * before it falls back to the plain dual loop, for the one-wave kernel (the paired kernel) and
+ * (*_wg) for the workgroup solver (overflow instances, the dense model; box-only problems);
+ * 0 / 0 where the dual loop starts cold.  Reported iterations count its working sets. */
+int mpcqp_ctx_crash_params(const mpcqp_ctx *ctx, int *kmax, int *pmax, int *kmax_wg,
+                           int *pmax_wg);
 
 /* Staged entry points (stage 1 / stage 2 below, mpcqp_batch_solve_qp): the stand-alone solve
  * holds 64 free variables per instance (more: per-instance status MPCQP_ERR_BAD_DIMS).  On a

@@ -182,6 +182,7 @@ __device__ __forceinline__ void dense_mpc_one(const MpcArgs &a, int b, unsigned 
     P.max_iter = a.max_iter;
     GiCtx C;
     C.wide = 1;
+    C.crash_p = a.crash_p_wg;
     C.stamps = a.stamps;
     C.cut = 0;
     C.P = &P;
@@ -478,7 +479,7 @@ __device__ __forceinline__ void dense_mpc_one(const MpcArgs &a, int b, unsigned 
     const double g = (ok && r < nf) ? fv[C.L.fid[r]] : 0.0;
     __syncthreads();  // the solver's workspace overlays the front
     MPCQP_STAMP(a.stamps, 3, tst);
-    gi_run_wg<NF>(C, hr, g, D + Lay::oU);
+    gi_run_wg<NF, true>(C, hr, g, D + Lay::oU);
     MPCQP_STAMP_INIT(tw);
     SolveOut O;
     O.x = a.U + (size_t)b * NV;

@@ -42,6 +42,8 @@ void add_dense(FastKernels &k) {
 
 bool pick_fast_dense(int nx, int nu, int N, bool toep, FastKernels &k) {
     if (nx == 24 && nu == 6 && N == 16) {  // config E
+        k.crash_k_wg = kWgCrashK;
+        k.crash_p_wg = kWgCrashP;
         if (toep && MPCQP_DENSE_TOEP) add_dense<24, 6, 16, true>(k);
         else add_dense<24, 6, 16, false>(k);
         return true;

@@ -39,6 +39,7 @@ struct FastKernels {
     int prim_nf = 0;  // free variables the one-wave kernel holds (kPairCap or its NF)
     int nf = 0;       // NF the one-wave kernel is instantiated for
     int crash_k = 0, crash_p = 0;  // the one-wave kernel's crash start (0: none)
+    int crash_k_wg = 0, crash_p_wg = 0;  // the workgroup solver's (overflow / dense kernels)
 };
 
 constexpr int kPairCap = 30;  // free variables of one half of the paired kernel (mpc_pair.hpp)

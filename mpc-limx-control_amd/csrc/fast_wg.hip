@@ -31,6 +31,9 @@ void add_wg(FastKernels &k) {
 
 bool add_fast_wg(int model, int N, bool fric, FastKernels &k) {
     if (model != MPCQP_MODEL_SRBM || k.nu != 6) return false;
+    // the crash start runs on box-only problems (no friction rows)
+    k.crash_k_wg = fric ? 0 : kWgCrashK;
+    k.crash_p_wg = fric ? 0 : kWgCrashP;
     if (N == 10) { fric ? add_wg<10, true, 64>(k) : add_wg<10, false, 64>(k); return true; }
     if (N == 20) { fric ? add_wg<20, true, 128>(k) : add_wg<20, false, 128>(k); return true; }
     return false;

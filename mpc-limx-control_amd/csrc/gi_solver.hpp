@@ -120,6 +120,7 @@ struct GiCtx {
     unsigned long long *stamps;  // diagnostic phase cycles (nullptr: off)
     int cut;                     // diagnostic cuts build only
     int wide;                    // 1: a workgroup solver (gi_wg.hpp) holds up to nfmax > 64
+    int crash_p;                 // workgroup solver: crash start's working sets (0: none)
 };
 
 __device__ __forceinline__ double rowA(const SolveProblem &P, int r, int v) {

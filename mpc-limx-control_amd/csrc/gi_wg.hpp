@@ -131,7 +131,210 @@ __device__ __forceinline__ void wg_pick(const double *red, int o, double &v, int
 #define MPCQP_WG_PDROP 1
 #endif
 
+// ---- crash start of the workgroup solver (box constraints only; the paired kernel's
+//      speculative primal-dual active-set start, mpc_pair.hpp / oracle box_crash, at the
+//      workgroup's scale).  Thread (r, 0) owns variable r's bounds and working-set state; the
+//      rows of J in A are published to the dead workspace, M = J_A J_A' is computed entry by
+//      entry over the whole workgroup (its lower triangle, mirrored), the k x k system by
+//      Gauss-Jordan over the workgroup (one barrier per pivot), y = J_A' w by column and
+//      dx = J y as each row's two half products.  Returns true when the working set settled (x,
+//      fval, iterations set, L.xs updated); false: nothing changed but the iteration count.
+#ifndef MPCQP_WG_CRASH_K
+#define MPCQP_WG_CRASH_K 32
+#endif
+#ifndef MPCQP_WG_CRASH_P
+#define MPCQP_WG_CRASH_P 12
+#endif
+constexpr int kWgCrashK = MPCQP_WG_CRASH_K, kWgCrashP = MPCQP_WG_CRASH_P;
+
 template <int NF>
+struct WgCrashLayout {
+    static constexpr int KC = kWgCrashK, RW = WgShape<NF>::RW;
+    static constexpr int LDW = NF + 1;  // odd row stride: the Gram's per-thread row reads
+    static constexpr int LDM = KC + 2;  // column KC: the right-hand side
+    static constexpr int oWr = 0, oM = oWr + KC * LDW, oW = oM + KC * LDM, oY = oW + KC;
+    static constexpr int oP = oY + NF, oR0 = oP + 2 * RW, oRed = oR0 + KC;
+    static constexpr int oRho = oRed + 16;  // int [RW]
+    static constexpr int doubles = oRho + RW / 2 + 1;
+};
+
+// rank of a flagged owner thread (h = 0: rows r = tid < RW, waves 0 .. NWH-1) among the flagged
+// ones in row order, and their count; one barrier
+template <int NWH>
+__device__ __forceinline__ int wg_rank(bool f, int *cnt, int wv, int ln, int &total) {
+    const uint64_t b = __ballot(f);
+    if (ln == 0) cnt[wv] = __popcll(b);
+    __syncthreads();
+    int base = 0;
+    total = 0;
+#pragma unroll
+    for (int w = 0; w < NWH; ++w) {
+        base += (w < wv) ? cnt[w] : 0;
+        total += cnt[w];
+    }
+    return base + __popcll(b & ((1ull << ln) - 1ull));
+}
+
+template <int NF>
+__device__ __forceinline__ bool wg_crash(GiCtx &C, const double (&Jr)[NF / 2], double &x,
+                                         double &fval, int &iters, double *W) {
+    using CL = WgCrashLayout<NF>;
+    static_assert(CL::doubles <= WgLayout<NF>::work, "the crash fits the solver's workspace");
+    constexpr int KC = CL::KC, NH = NF / 2, RW = WgShape<NF>::RW, NWH = WgShape<NF>::NWH;
+    constexpr int NT = 2 * RW, LDW = CL::LDW, LDM = CL::LDM;
+    GiLds &L = C.L;
+    const WgIds T = wg_ids<RW>();
+    const int h = T.h, r = T.r, wv = T.wv, ln = T.ln, tid = T.tid, nf = C.nf, PC = C.crash_p;
+    double *Wr = W + CL::oWr, *M = W + CL::oM, *Wv = W + CL::oW, *Yv = W + CL::oY,
+           *Pp = W + CL::oP, *R0 = W + CL::oR0, *red = W + CL::oRed;
+    int *rho_of = reinterpret_cast<int *>(W + CL::oRho);
+    int *cnt = reinterpret_cast<int *>(red + 8);
+    const bool owner = h == 0 && r < nf;
+    double b0 = 0.0, b1 = 0.0;
+    int s0 = 0, s1 = 0;
+    if (owner) {
+        s0 = L.st[r];
+        s1 = L.st[r + nf];
+        b0 = L.cb[r];
+        b1 = L.cb[r + nf];
+    }
+    const double x0 = x, f0 = fval;
+    double xc = x0, lam = 0.0, fc = f0;
+    int side = 0, cit = 0, solves = 0;
+    bool settled = false;
+    for (;;) {
+        int nw = side;
+        if (owner) {
+            if (side == 0) {
+                if (s0 == 1 && xc - b0 < -kFeasTol * (1.0 + fabs(b0))) nw = 1;
+                else if (s1 == 1 && -xc - b1 < -kFeasTol * (1.0 + fabs(b1))) nw = -1;
+            } else if (lam < 0.0) {
+                nw = 0;
+            }
+        }
+        if (!__syncthreads_or(owner && nw != side)) { settled = true; break; }
+        if (cit >= PC) break;  // give up
+        {   // at most KC bounds: those already in A, then the lowest variable ids
+            int tot = 0, kept = 0;
+            (void)wg_rank<NWH>(owner && nw != 0, cnt, wv, ln, tot);
+            __syncthreads();
+            if (tot > KC) {
+                (void)wg_rank<NWH>(owner && nw != 0 && side != 0, cnt, wv, ln, kept);
+                __syncthreads();
+                int nadd = 0;
+                const int rk = wg_rank<NWH>(owner && nw != 0 && side == 0, cnt, wv, ln, nadd);
+                __syncthreads();
+                if (owner && nw != 0 && side == 0 && rk >= KC - kept) nw = 0;
+            }
+        }
+        if (owner) side = nw;
+        ++cit;
+        const bool inA = owner && side != 0;
+        int k = 0;
+        const int rho = wg_rank<NWH>(inA, cnt, wv, ln, k);
+        if (k == 0) {  // (workgroup-uniform) the unconstrained minimum again
+            xc = x0;
+            lam = 0.0;
+            fc = f0;
+            __syncthreads();
+            continue;
+        }
+        ++solves;
+        const double bv = side > 0 ? b0 : -b1;
+        if (h == 0) rho_of[r] = inA ? rho : -1;
+        if (inA) {
+            R0[rho] = x0 - bv;
+            M[rho * LDM + KC] = x0 - bv;
+        }
+        __syncthreads();
+        {   // publish the J rows of A (both halves of each row)
+            const int rr = (r < nf) ? rho_of[r] : -1;
+            if (rr >= 0) {
+#pragma unroll
+                for (int j = 0; j < NH; ++j) Wr[rr * LDW + h * NH + j] = Jr[j];
+            }
+        }
+        __syncthreads();
+        // M = J_A J_A': lower-triangle entries over the workgroup, mirrored
+        const int ne = k * (k + 1) / 2;
+        for (int e = tid; e < ne; e += NT) {
+            int i = (int)((__builtin_sqrtf(8.0f * (float)e + 1.0f) - 1.0f) * 0.5f);
+            i += ((i + 1) * (i + 2) / 2 <= e) ? 1 : 0;
+            i -= (i * (i + 1) / 2 > e) ? 1 : 0;
+            const int m = e - i * (i + 1) / 2;
+            const double *wi = Wr + i * LDW, *wm = Wr + m * LDW;
+            double s4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int c = 0; c < NF; ++c) {
+                s4[c & 3] += wi[c] * wm[c];
+                if ((c & 15) == 15) step_fence();
+            }
+            const double sv = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+            M[i * LDM + m] = sv;
+            M[m * LDM + i] = sv;
+        }
+        __syncthreads();
+        // Gauss-Jordan without pivoting (M positive definite), one barrier per pivot: step j
+        // writes M(i, m) for i != j, m > j (and the right-hand side) and reads only column j and
+        // row j, which it does not write
+        bool bad = false;
+        for (int j = 0; j < k; ++j) {
+            const double d = M[j * LDM + j];
+            bad |= !(d > 0.0);
+            const double inv = 1.0 / d;
+            const int ncol = k - j;  // columns j+1 .. k-1, then the right-hand side
+            for (int e = tid; e < (k - 1) * ncol; e += NT) {
+                const int ii = e / ncol, mm = e - ii * ncol;
+                const int i = ii + (ii >= j ? 1 : 0), m = (mm < ncol - 1) ? j + 1 + mm : KC;
+                const double l = M[i * LDM + j] * inv;
+                M[i * LDM + m] -= l * M[j * LDM + m];
+            }
+            __syncthreads();
+        }
+        if (bad) break;  // (workgroup-uniform: every thread read the same pivots) give up
+        if (tid < k) Wv[tid] = M[tid * LDM + KC] / M[tid * LDM + tid];
+        __syncthreads();
+        // y = J_A' w by column; f = f0 + w'(x0_A - b_A) / 2
+        if (tid < NF) {
+            double y = 0.0;
+            for (int m = 0; m < k; ++m) y += Wr[m * LDW + tid] * Wv[m];
+            Yv[tid] = y;
+        }
+        if (wv == NWH * 2 - 1) {
+            double s = 0.0;
+            for (int m = ln; m < k; m += 64) s += Wv[m] * R0[m];
+            s = wave_sum(s);
+            if (ln == 0) red[0] = s;
+        }
+        __syncthreads();
+        {   // dx = J y: each row's two half products
+            double s4[4] = {0.0, 0.0, 0.0, 0.0};
+            const double *yv = Yv + h * NH;
+#pragma unroll
+            for (int j = 0; j < NH; ++j) {
+                s4[j & 3] += Jr[j] * yv[j];
+                if ((j & 7) == 7) step_fence();
+            }
+            Pp[h * RW + r] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+        }
+        __syncthreads();
+        if (owner) {
+            xc = inA ? bv : x0 - (Pp[r] + Pp[RW + r]);
+            lam = inA ? -(double)side * Wv[rho] : 0.0;
+        }
+        fc = f0 + 0.5 * red[0];
+        __syncthreads();
+    }
+    iters = solves;
+    if (!settled) return false;
+    if (owner) L.xs[r] = xc;
+    __syncthreads();
+    x = (r < nf) ? L.xs[r] : 0.0;
+    fval = fc;
+    return true;
+}
+
+template <int NF, bool CRASH = false>
 __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double g, double *W) {
     using Lay = WgLayout<NF>;
     constexpr int NH = Lay::NH, CBW = Lay::CBW, RW = Lay::RW, NWH = WgShape<NF>::NWH;
@@ -219,6 +422,11 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
     // ---- dual active-set loop: one pass = one add or drop step
     const int max_iter = P.max_iter > 0 ? P.max_iter : 10 * (mt + nf + 1);
     bool done = (status != ST_OK) || nf == 0;
+    if constexpr (CRASH) {
+        // (workgroup-uniform condition: status, nf and the problem kind are the instance's)
+        if (!done && C.nfric == 0 && C.crash_p > 0) done = wg_crash<NF>(C, Jr, x, fval, iters, W);
+    }
+    MPCQP_CUT(C.cut, 8);
     bool fresh = true;
     int p = 0;
     int fbase = -1;  // friction rows of the foot-step whose vertical force is variable r

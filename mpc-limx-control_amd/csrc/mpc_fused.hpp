@@ -46,6 +46,7 @@ struct MpcArgs {
     double fz_min, fz_max, fxy_max, u_min, u_max, mu;
     int max_iter, max_free;
     int crash_p;  // paired kernel: working sets of its crash start before the dual loop (0: none)
+    int crash_p_wg;  // the workgroup solver's (gi_wg.hpp), box-only problems
     // paired kernel's bound constants, by kind of free variable (v: a vertical force, t: a
     // tangential force; the literal model's inputs use v): b of x >= lo (lo) and of -x >= -hi
     // (-hi), and the dual loop's violation thresholds -kFeasTol (1 + |b|), precomputed on the

@@ -448,6 +448,9 @@ bool pick_fast(int model, int nx, int nu, int N, bool fric, int nfmax, FastKerne
     // working sets (0: the plain dual loop from the unconstrained minimum; A/B runs and tests)
     if (k.pair && k.crash_k > 0)
         if (const char *e = getenv("MPCQP_CRASH_P")) k.crash_p = std::max(0, atoi(e));
+    // MPCQP_CRASH_P_WG=n: the same for the workgroup solver (overflow / dense kernels)
+    if (k.crash_k_wg > 0)
+        if (const char *e = getenv("MPCQP_CRASH_P_WG")) k.crash_p_wg = std::max(0, atoi(e));
     if (found) {
         k.prim_nf = k.pair ? kPairCap : k.nf;
         if (nfmax > k.prim_nf) add_fast_wg(model, N, fric, k);
@@ -955,6 +958,7 @@ int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
         if (pick_fast_dense(nx, nu, m->N, toep, c->fk)) {
             c->fast = true;
             set_lds(c->fk.dense, c->fk.dense_lds);
+            if (const char *e = getenv("MPCQP_CRASH_P_WG")) c->fk.crash_p_wg = std::max(0, atoi(e));
         }
     }
     if (!c->fast && nfmax > kWave) {  // the generic one-wave solver holds 64 free variables
@@ -984,11 +988,15 @@ int mpcqp_ctx_one_wave_nf(const mpcqp_ctx *c) {
     return c->fk.prim_nf;
 }
 
-int mpcqp_ctx_crash_params(const mpcqp_ctx *c, int *kmax, int *pmax) {
-    if (!c || !kmax || !pmax) return MPCQP_ERR_BAD_ARG;
+int mpcqp_ctx_crash_params(const mpcqp_ctx *c, int *kmax, int *pmax, int *kmax_wg,
+                           int *pmax_wg) {
+    if (!c || !kmax || !pmax || !kmax_wg || !pmax_wg) return MPCQP_ERR_BAD_ARG;
     const bool on = c->fast && c->fk.pair && !c->fk.dense;
     *kmax = on ? c->fk.crash_k : 0;
     *pmax = on ? c->fk.crash_p : 0;
+    const bool wg = c->fast && (c->fk.wg || c->fk.dense);
+    *kmax_wg = wg ? c->fk.crash_k_wg : 0;
+    *pmax_wg = wg ? c->fk.crash_p_wg : 0;
     return MPCQP_OK;
 }
 
@@ -1186,6 +1194,7 @@ static MpcArgs mpc_args(mpcqp_ctx *c, int B) {
     a.max_iter = m.max_iter;
     a.max_free = m.max_free > 0 ? m.max_free : m.nu * m.N;
     a.crash_p = c->fk.crash_p;
+    a.crash_p_wg = c->fk.crash_p_wg;
     {   // (pair_mpc's bound selection; gi_solver.hpp kFeasTol)
         const bool lit = m.model == MPCQP_MODEL_LITERAL;
         a.blo_v = lit ? m.u_min : m.fz_min;

@@ -79,7 +79,7 @@ def lib():
     L.mpcqp_batch_solve_qp.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp]
     L.mpcqp_batch_solve.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp]
     L.mpcqp_ctx_fast_path.argtypes = [vp]
-    for name, at in (("mpcqp_ctx_one_wave_nf", [vp]), ("mpcqp_ctx_crash_params", [vp, vp, vp])):
+    for name, at in (("mpcqp_ctx_one_wave_nf", [vp]), ("mpcqp_ctx_crash_params", [vp] + [vp] * 4)):
         if hasattr(L, name):  # absent from A/B builds of older sources
             getattr(L, name).argtypes = at
     L.mpcqp_debug_phase_cycles.argtypes = [vp, vp, i]

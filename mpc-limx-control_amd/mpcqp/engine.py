@@ -101,15 +101,19 @@ class BatchEngine:
 
     @property
     def crash(self) -> tuple:
-        """(bounds per working set, working sets) of the one-wave kernel's crash start, (0, 0)
-        if none: the oracle reproduces its iteration counts with p["crash"] set to this"""
+        """(kmax, pmax) of the one-wave kernel's crash start, (kmax, pmax) of the workgroup
+        solver's, and the free count above which an instance is the workgroup solver's; zeros
+        where the dual loop starts cold.  The oracle reproduces the iteration counts with
+        p["crash"] set to this tuple."""
         import ctypes as C
         if not hasattr(lib(), "mpcqp_ctx_crash_params"):  # an A/B build of older sources
-            return (0, 0)
-        k, n = C.c_int(0), C.c_int(0)
-        check("mpcqp_ctx_crash_params", lib().mpcqp_ctx_crash_params(self.ctx, C.byref(k),
-                                                                       C.byref(n)))
-        return (k.value, n.value)
+            return (0, 0, 0, 0, 0)
+        v = [C.c_int(0) for _ in range(4)]
+        check("mpcqp_ctx_crash_params",
+              lib().mpcqp_ctx_crash_params(self.ctx, *[C.byref(x) for x in v]))
+        # (one-wave kmax, pmax, workgroup kmax, pmax, the free count above which an instance is
+        #  the workgroup solver's)
+        return tuple(x.value for x in v) + (self.pair_nf,)
 
     @property
     def fused_kernel(self) -> str:

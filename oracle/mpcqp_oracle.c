@@ -1042,8 +1042,12 @@ static int srbm_one(const orc_srbm_cfg *cfg, const double *x0, const double *xre
                  NULL, NULL, NULL, NULL, NULL, NULL, NULL);
     orc_srbm_bounds(cfg, contact, lb, ub);
     orc_friction fr = {cfg->friction && cfg->model == 0, nu, N, 2, cfg->mu, contact};
+    int nfree = 0;
+    for (int v = 0; v < nV; ++v) nfree += lb[v] != ub[v];
+    const int wg = nfree > cfg->crash_split;
     int st = solve_qp_impl(nV, H, f, 0, NULL, 0, lb, ub, NULL, NULL, &fr, cfg->max_iter, U,
-                           cost, iters, NULL, NULL, cfg->crash_kmax, cfg->crash_pmax);
+                           cost, iters, NULL, NULL, wg ? cfg->crash_kmax_wg : cfg->crash_kmax,
+                           wg ? cfg->crash_pmax_wg : cfg->crash_pmax);
     if (!Hout) free(H);
     if (!fout) free(f);
     free(lb);

@@ -111,8 +111,9 @@ typedef struct {
     int max_iter;
     /* bounds-only problems: the GPU kernels' speculative primal-dual active-set start (at most
      * crash_kmax bounds per working set, crash_pmax working sets, then Goldfarb-Idnani);
-     * 0 = off (plain Goldfarb-Idnani, the solve every other path runs) */
-    int crash_kmax, crash_pmax;
+     * 0 = off (plain Goldfarb-Idnani, the solve every other path runs).  Instances with more
+     * than crash_split free variables are the workgroup solver's: crash_kmax_wg / _pmax_wg. */
+    int crash_kmax, crash_pmax, crash_kmax_wg, crash_pmax_wg, crash_split;
 } orc_srbm_cfg;
 
 /* x0: [B][nx]; xref: [B][N+1][nx]; lin: [B][8]; contact: [B]; U: [B][nu*N] */

@@ -35,7 +35,17 @@ class SrbmCfg(C.Structure):
                 ("fz_max", C.c_double), ("fxy_max", C.c_double), ("u_min", C.c_double),
                 ("u_max", C.c_double), ("Q", C.c_void_p), ("R", C.c_void_p),
                 ("P", C.c_void_p), ("max_iter", C.c_int), ("crash_kmax", C.c_int),
-                ("crash_pmax", C.c_int)]
+                ("crash_pmax", C.c_int), ("crash_kmax_wg", C.c_int), ("crash_pmax_wg", C.c_int),
+                ("crash_split", C.c_int)]
+
+
+def crash_params(p):
+    """p["crash"]: the library's (kmax, pmax, kmax_wg, pmax_wg, split) (BatchEngine.crash), or a
+    (kmax, pmax) pair for every instance; absent: the plain dual loop"""
+    c = tuple(p.get("crash", (0, 0)))
+    if len(c) == 2:
+        return c + (c[0], c[1], 1 << 30)
+    return c
 
 
 def build() -> str:
@@ -200,7 +210,8 @@ def make_cfg(p):
     keep = [_f(p["Q"]), _f(p["R"]), _f(p["P"])]
     cfg.Q, cfg.R, cfg.P = [k.ctypes.data for k in keep]
     cfg.max_iter = p.get("max_iter", 0)
-    cfg.crash_kmax, cfg.crash_pmax = p.get("crash", (0, 0))
+    (cfg.crash_kmax, cfg.crash_pmax, cfg.crash_kmax_wg, cfg.crash_pmax_wg,
+     cfg.crash_split) = crash_params(p)
     return cfg, keep
 
 
@@ -272,7 +283,7 @@ def dense_batch(p, x0, xref, AB, nthreads=0, want_hf=False):
     """config E (dense continuous model per instance): discretize -> literal dense condensing ->
     box-constrained Goldfarb-Idnani.  AB [B, nx*(nx+nu)] = [Ac | Bc] column-major."""
     keep = [_f(p["Q"]), _f(p["R"]), _f(p["P"])]
-    ck, cp = p.get("crash", (0, 0))
+    _, _, ck, cp, _ = crash_params(p)  # the dense model runs the workgroup solver
     cfg = DenseCfg(p["nx"], p["nu"], p["N"], p["Ts"], keep[0].ctypes.data, keep[1].ctypes.data,
                    keep[2].ctypes.data, p["u_min"], p["u_max"], p.get("max_iter", 0), ck, cp)
     B = int(x0.shape[0])

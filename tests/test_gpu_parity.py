@@ -577,20 +577,25 @@ def test_overflow_workgroup_kernel_vs_oracle(gpu, orc, config, B):
     assert (nfree > cap).sum() > B // 5 and (nfree <= cap).sum() > B // 5
     assert nfree.max() == 6 * p["N"]  # standing candidates
     eng = BatchEngine(p)
+    crash = eng.crash
     d = _prefilled(eng, batch)
     eng.solve(d)
     eng.sync()
     o = {k: d[k].cpu().numpy() for k in ("U", "cost", "status", "iters")}
     eng.close()
     ref = orc.srbm_batch(p, batch["x0"], batch["xref"], batch["lin"], ct)
+    refc = orc.srbm_batch(with_crash(p, crash), batch["x0"], batch["xref"], batch["lin"], ct)
     assert np.all(ref["status"] == 0)
     np.testing.assert_array_equal(o["status"], ref["status"])
     assert np.all(np.isfinite(o["U"])) and np.all(o["iters"] >= 0)
     bad = [i for i in range(B) if not u_close(o["U"][i], ref["U"][i])]
     assert not bad, (bad[:10], nfree[bad[:10]])
     np.testing.assert_allclose(o["cost"], ref["cost"], rtol=1e-9, atol=1e-9)
+    # iteration counts: the workgroup solver's crash start (box-only problems: config B) and
+    # the oracle run with the same caps
+    assert (crash[2] > 0) == (config == "B")
     big = nfree > cap
-    assert np.mean(o["iters"][big] == ref["iters"][big]) >= 0.95
+    assert np.mean(o["iters"][big] == refc["iters"][big]) >= 0.95
 
 
 def test_overflow_full_size_mixed_gait(gpu, orc):
@@ -693,6 +698,7 @@ def test_dense_fused_vs_oracle(gpu, orc):
     batch = mpcqp.make_batch(p, B, seed=9)
     eng = BatchEngine(p)
     assert eng.fused_kernel == "k_dense_wg"
+    crash = eng.crash
     d = _prefilled(eng, batch)
     eng.solve(d)
     eng.sync()
@@ -705,7 +711,10 @@ def test_dense_fused_vs_oracle(gpu, orc):
     bad = [i for i in range(B) if not u_close(o["U"][i], ref["U"][i])]
     assert not bad, bad[:10]
     np.testing.assert_allclose(o["cost"], ref["cost"], rtol=1e-9, atol=1e-9)
-    assert np.mean(o["iters"] == ref["iters"]) >= 0.95
+    # iteration counts against the oracle run with the workgroup solver's crash start
+    assert crash[2] > 0
+    refc = orc.dense_batch(with_crash(p, crash), batch["x0"], batch["xref"], batch["lin"])
+    assert np.mean(o["iters"] == refc["iters"]) >= 0.95
 
 
 def test_dense_full_weights_vs_oracle(gpu, orc):
@@ -829,3 +838,38 @@ def test_pair_crash_fallback_paths(gpu, orc, monkeypatch, crash_p):
         assert np.mean(o["iters"] == plain["iters"]) >= 0.99
     else:  # some instances fell back: more iterations than working sets
         assert (o["iters"] > int(crash_p)).any()
+
+
+@pytest.mark.parametrize("crash_p", ["0", "1"])
+def test_wg_crash_fallback_paths(gpu, orc, monkeypatch, crash_p):
+    """the workgroup solver's crash start capped at 0 / 1 working sets (MPCQP_CRASH_P_WG) at B
+    standing (every instance in the overflow kernel, NF = 64) and config E (NF = 96): 0 is the
+    plain dual loop, 1 gives up on most instances; U / cost equal the oracle's optimum, the
+    iteration counts the oracle run with the same caps"""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    monkeypatch.setenv("MPCQP_CRASH_P_WG", crash_p)
+    for config, gait, B in (("B", "standing", 256), ("E", None, 96)):
+        p = mpcqp.model_params(config)
+        batch = mpcqp.make_batch(p, B, seed=53, gait=gait) if gait else \
+            mpcqp.make_batch(p, B, seed=53)
+        eng = BatchEngine(p)
+        crash = eng.crash
+        assert crash[3] == int(crash_p)
+        d = _prefilled(eng, batch)
+        eng.solve(d)
+        eng.sync()
+        o = {k: d[k].cpu().numpy() for k in ("U", "cost", "status", "iters")}
+        eng.close()
+        args = (batch["x0"], batch["xref"], batch["lin"]) if config == "E" else \
+            (batch["x0"], batch["xref"], batch["lin"], batch["contact"])
+        fn = orc.dense_batch if config == "E" else orc.srbm_batch
+        ref = fn(p, *args)
+        refc = fn(with_crash(p, crash), *args)
+        assert np.all(o["status"] == 0) and np.all(ref["status"] == 0)
+        bad = [i for i in range(B) if not u_close(o["U"][i], ref["U"][i])]
+        assert not bad, (config, bad[:10])
+        np.testing.assert_allclose(o["cost"], ref["cost"], rtol=1e-9, atol=1e-9)
+        assert np.mean(o["iters"] == refc["iters"]) >= 0.95, config
+        if crash_p == "0":
+            assert np.mean(o["iters"] == ref["iters"]) >= 0.95, config
