@@ -448,13 +448,13 @@ bool pick_fast(int model, int nx, int nu, int N, bool fric, int nfmax, FastKerne
     // working sets (0: the plain dual loop from the unconstrained minimum; A/B runs and tests)
     if (k.pair && k.crash_k > 0)
         if (const char *e = getenv("MPCQP_CRASH_P")) k.crash_p = std::max(0, atoi(e));
-    // MPCQP_CRASH_P_WG=n: the same for the workgroup solver (overflow / dense kernels)
-    if (k.crash_k_wg > 0)
-        if (const char *e = getenv("MPCQP_CRASH_P_WG")) k.crash_p_wg = std::max(0, atoi(e));
     if (found) {
         k.prim_nf = k.pair ? kPairCap : k.nf;
         if (nfmax > k.prim_nf) add_fast_wg(model, N, fric, k);
     }
+    // MPCQP_CRASH_P_WG=n: the same for the workgroup solver (overflow / dense kernels)
+    if (k.crash_k_wg > 0)
+        if (const char *e = getenv("MPCQP_CRASH_P_WG")) k.crash_p_wg = std::max(0, atoi(e));
     return found;
 }
 

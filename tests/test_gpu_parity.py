@@ -426,7 +426,7 @@ def test_pair_kernel_matches_single_and_oracle(gpu, orc, monkeypatch):
     assert np.all(pair["status"][bad_dims] == 1) and np.all(pair["status"][~bad_dims] == 0)
     # iteration counts: the one-QP kernel runs the plain dual loop, the paired kernel its crash
     # start first -- each against the oracle configured the same way (below)
-    assert single["crash"] == (0, 0) and pair["crash"][0] > 0
+    assert single["crash"][:2] == (0, 0) and pair["crash"][0] > 0
     # blocked MFMA factorisation in the one-QP kernel vs column sweeps in the paired one
     sc = np.maximum(1.0, np.abs(single["U"]).max(axis=1, keepdims=True))
     assert np.all(np.abs(pair["U"] - single["U"]) <= 1e-10 * sc)

@@ -19,6 +19,9 @@ ap.add_argument("--gait", default="alternating")
 ap.add_argument("--batches", default="512,4096,8192,65536")
 ap.add_argument("--rounds", type=int, default=8)
 ap.add_argument("--per", type=int, default=16)
+ap.add_argument("--slot", type=int, default=2,
+                help="library timing slot: 2 the one-wave kernel, 3 the workgroup kernel, 1 the "
+                     "whole solve call (dense contexts: 1)")
 args = ap.parse_args()
 import mpcqp  # noqa: E402
 from mpcqp.engine import BatchEngine  # noqa: E402
@@ -40,14 +43,14 @@ for B in [int(b) for b in args.batches.split(",")]:
         for _ in range(40):
             e.solve(d)
         e.sync()
-        e.kernel_ms_sum(2)
+        e.kernel_ms_sum(args.slot)
     res = {spec: [] for spec, _, _ in engs}
     for _ in range(args.rounds):
         for spec, e, d in engs:
             for _ in range(args.per):
                 e.solve(d)
             e.sync()
-            ms, n = e.kernel_ms_sum(2)
+            ms, n = e.kernel_ms_sum(args.slot)
             res[spec].append(ms / max(1, n))
     line = [f"{args.config}@{B} ({args.gait})"]
     for spec, e, d in engs:
