@@ -728,7 +728,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         //      chunk's LDS reads issued together); past-k entries of a chunk are computed from
         //      clamped addresses and never read.
         {
-            constexpr int KC = kPairCrashK, CH = 4;
+            constexpr int KC = kPairCrashK, CH = 2;
             static_assert(KC % CH == 0, "whole chunks");
             const int PC = a.crash_p;
             static_assert(KC * NF <= Lay::NR, "the published J rows fit the dead L space");
@@ -808,23 +808,38 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         #pragma unroll
                 for (int j = 0; j < KC; ++j) {
                     if (j < kmax) {
+                        // (columns past kmax are never read: the row's tail goes in chunks of
+                        //  four behind wave-uniform guards)
                         if (inA && rho == j) {
         #pragma unroll
-                            for (int m = j; m < KC; ++m) Pv[m] = Mr[m];
+                            for (int m0 = j & ~3; m0 < KC; m0 += 4) {
+                                if (m0 < kmax) {
+        #pragma unroll
+                                    for (int m = m0; m < m0 + 4; ++m)
+                                        if (m >= j) Pv[m] = Mr[m];
+                                }
+                            }
                             Pv[KC] = rr;
                             Pv[KC + 1] = 1.0 / Mr[j];
                             dd = Mr[j];
                             bad |= !(Mr[j] > 0.0);
                         }
                         wave_sync();
-                        double pv[KC + 2];
+                        const double pr = Pv[KC], pi = Pv[KC + 1];
+                        double pv[KC];
         #pragma unroll
-                        for (int m = j + 1; m < KC + 2; ++m) pv[m] = Pv[m];
+                        for (int m = j + 1; m < KC; ++m) pv[m] = Pv[m];
                         if (inA && rho != j && j < k) {
-                            const double l = Mr[j] * pv[KC + 1];
+                            const double l = Mr[j] * pi;
         #pragma unroll
-                            for (int m = j + 1; m < KC; ++m) Mr[m] -= l * pv[m];
-                            rr -= l * pv[KC];
+                            for (int m0 = (j + 1) & ~3; m0 < KC; m0 += 4) {
+                                if (m0 < kmax) {
+        #pragma unroll
+                                    for (int m = m0; m < m0 + 4; ++m)
+                                        if (m > j) Mr[m] -= l * pv[m];
+                                }
+                            }
+                            rr -= l * pr;
                         }
                     }
                 }
@@ -833,7 +848,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 if (inA) Wv[rho] = w;
                 wave_sync();
                 // y = J_A' w (lane c: column c of the published rows), then x = x0 - J y
-                double yv[CH] = {0.0, 0.0, 0.0, 0.0};
+                double yv[CH] = {};
                 const int cc = hl < NF ? hl : 0;
         #pragma unroll
                 for (int m0 = 0; m0 < KC; m0 += CH) {
@@ -845,7 +860,10 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                         }
                     }
                 }
-                if (hl < NF) Yv[hl] = (yv[0] + yv[1]) + (yv[2] + yv[3]);
+                double ys = 0.0;
+        #pragma unroll
+                for (int m = 0; m < CH; ++m) ys += yv[m];
+                if (hl < NF) Yv[hl] = ys;
                 wave_sync();
                 double s4[4] = {0.0, 0.0, 0.0, 0.0};
         #pragma unroll
