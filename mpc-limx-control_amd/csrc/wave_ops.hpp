@@ -216,11 +216,14 @@ __device__ __forceinline__ void step_fence() {
 
 // 1/sqrt(a) for a > 0: v_rsq_f64 plus two Newton steps (~1 ulp; a short dependency chain
 // compared with the correctly rounded sqrt and divide sequences)
+#ifndef MPCQP_RSQ_NR
+#define MPCQP_RSQ_NR 2  // Newton steps after v_rsq_f64 (A/B builds: 1)
+#endif
 __device__ __forceinline__ double rsqrt_nr(double a) {
     double y = __builtin_amdgcn_rsq(a);
     const double h = 0.5 * a;
-    y = y * fma(-h * y, y, 1.5);
-    y = y * fma(-h * y, y, 1.5);
+#pragma unroll
+    for (int i = 0; i < MPCQP_RSQ_NR; ++i) y = y * fma(-h * y, y, 1.5);
     return y;
 }
 
