@@ -184,7 +184,7 @@ __device__ __forceinline__ void dense_mpc_one(const MpcArgs &a, int b, unsigned 
     C.wide = 1;
     C.crash_p = a.crash_p_wg;
     C.stamps = a.stamps;
-    C.cut = 0;
+    C.cut = a.cut >= 100 ? a.cut - 100 : 0;  // (cuts build) MPCQP_CUT=100+k: the workgroup solver's cut k
     C.P = &P;
     C.nfmax = NF;
     C.L.ld = NF | 1;

@@ -31,9 +31,12 @@ void add_wg(FastKernels &k) {
 
 bool add_fast_wg(int model, int N, bool fric, FastKernels &k) {
     if (model != MPCQP_MODEL_SRBM || k.nu != 6) return false;
-    // the crash start runs on box-only problems (no friction rows)
-    k.crash_k_wg = fric ? 0 : kWgCrashK;
-    k.crash_p_wg = fric ? 0 : kWgCrashP;
+    // the crash start runs on box-only problems (no friction rows), and in these kernels only
+    // when built with MPCQP_WG_SRBM_CRASH=1: at B standing its working sets average 21 bounds,
+    // and their solves cost more than the dual passes they replace
+    const bool crash = !fric && MPCQP_WG_SRBM_CRASH;
+    k.crash_k_wg = crash ? kWgCrashK : 0;
+    k.crash_p_wg = crash ? kWgCrashP : 0;
     if (N == 10) { fric ? add_wg<10, true, 64>(k) : add_wg<10, false, 64>(k); return true; }
     if (N == 20) { fric ? add_wg<20, true, 128>(k) : add_wg<20, false, 128>(k); return true; }
     return false;

@@ -146,6 +146,9 @@ __device__ __forceinline__ void wg_pick(const double *red, int o, double &v, int
 #define MPCQP_WG_CRASH_P 12
 #endif
 constexpr int kWgCrashK = MPCQP_WG_CRASH_K, kWgCrashP = MPCQP_WG_CRASH_P;
+#ifndef MPCQP_WG_SRBM_CRASH
+#define MPCQP_WG_SRBM_CRASH 0  // the SRBM overflow kernels (mpc_wg.hpp) without the crash
+#endif
 
 template <int NF>
 struct WgCrashLayout {

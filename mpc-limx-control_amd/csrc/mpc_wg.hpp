@@ -73,9 +73,9 @@ __device__ __forceinline__ void wg_mpc_one(const MpcArgs &a, int b, unsigned cha
     P.max_iter = a.max_iter;
     GiCtx C;
     C.wide = 1;
-    C.crash_p = FRIC ? 0 : a.crash_p_wg;
+    C.crash_p = (FRIC || !MPCQP_WG_SRBM_CRASH) ? 0 : a.crash_p_wg;
     C.stamps = a.stamps;
-    C.cut = 0;
+    C.cut = a.cut >= 100 ? a.cut - 100 : 0;  // (cuts build) MPCQP_CUT=100+k: the workgroup solver's cut k
     MPCQP_STAMP_INIT(tst);
     C.P = &P;
     C.nfmax = NF;
@@ -133,7 +133,7 @@ __device__ __forceinline__ void wg_mpc_one(const MpcArgs &a, int b, unsigned cha
     }
     __syncthreads();  // the solver's workspace overlays the condensed terms
     MPCQP_STAMP(a.stamps, 3, tst);
-    gi_run_wg<NF, !FRIC>(C, hr, g, D + Lay::oW);
+    gi_run_wg<NF, !FRIC && MPCQP_WG_SRBM_CRASH>(C, hr, g, D + Lay::oW);
     MPCQP_STAMP_INIT(tw);
     SolveOut O;
     O.x = a.U + (size_t)b * NV;
