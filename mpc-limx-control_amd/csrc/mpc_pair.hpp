@@ -196,6 +196,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     if constexpr (MPCQP_PAIR_SORT && MODEL == 0) bq = pair_sorted_instance<GEN>(a);
     const bool valid = bq < a.B;
     const int b = valid ? bq : a.B - 1;  // the spare half of an odd batch re-reads the last QP
+    [[maybe_unused]] const int b_ = b;
     double *D = reinterpret_cast<double *>(smem + (up ? Lay::bytes : 0));
     int *fid = reinterpret_cast<int *>(D + Lay::nDoubles);
     int *pos = fid + NF;
@@ -238,6 +239,11 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         }
         contact = gait_mask_half(N, a.Ts, ph0, a.swing, a.stance);
     } else {
+        // (diagnostic MPCQP_INPUT_ALIAS=n: inputs of instance b mod n, L2-resident -- the
+        //  kernel time without the input loads' HBM latency; results are not the batch's)
+#ifdef MPCQP_INPUT_ALIAS
+        const int b = b_ % MPCQP_INPUT_ALIAS;
+#endif
 #pragma unroll
         for (int i = 0; i < 8; ++i) lin[i] = stream_load(a.lin + (size_t)b * 8 + i);
         constexpr int NXR = NX * (N + 1), RX = (NXR + kHalf - 1) / kHalf;
