@@ -21,8 +21,20 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--warmup", type=int, default=5)
 ap.add_argument("--batch", type=int, default=65536)
+ap.add_argument("--preheat", default="", help="before the profiled engine: 'same-kernel' (the "
+                "headline on another engine and batch) or a config name (C, E), for ~1 s")
 args = ap.parse_args()
 p = mpcqp.model_params("B")
+if args.preheat:
+    cfg = "B" if args.preheat == "same-kernel" else args.preheat
+    pp = mpcqp.model_params(cfg)
+    e2 = BatchEngine(pp)
+    d2 = e2.upload(mpcqp.make_batch(pp, 65536 if cfg != "E" else 16384, seed=99))
+    t1 = time.perf_counter()
+    while time.perf_counter() - t1 < 1.0:
+        e2.solve(d2)
+        e2.sync()
+    e2.close()
 eng = BatchEngine(p)
 d = eng.upload(mpcqp.make_batch(p, args.batch))
 rec = torch.zeros(1 + p["nu"] * p["N"], dtype=torch.int64, device="cuda")
