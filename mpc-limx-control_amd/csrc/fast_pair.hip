@@ -3,12 +3,6 @@
 // and the reference-literal 13/3/10.
 #include <hip/hip_runtime.h>
 
-// one Newton step after v_rsq_f64 for the Cholesky pivots of the paired kernel (the other
-// kernels keep two): parity unchanged, 315 -> 311 us at B
-#ifndef MPCQP_RSQ_NR
-#define MPCQP_RSQ_NR 1
-#endif
-
 #include "../../include/mpcqp.h"
 #include "fast_kernels.hpp"
 #include "mpc_pair.hpp"

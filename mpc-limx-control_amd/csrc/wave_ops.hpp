@@ -217,7 +217,10 @@ __device__ __forceinline__ void step_fence() {
 // 1/sqrt(a) for a > 0: v_rsq_f64 plus two Newton steps (~1 ulp; a short dependency chain
 // compared with the correctly rounded sqrt and divide sequences)
 #ifndef MPCQP_RSQ_NR
-#define MPCQP_RSQ_NR 2  // Newton steps after v_rsq_f64 (A/B builds: 1)
+// Newton steps after v_rsq_f64 (its estimate is good to about half the mantissa; one step squares
+// the error): 1 since r04 -- parity suite unchanged, B 315 -> 311 us, L 2.38 -> 2.34 ms,
+// C / E -0.5..0.8 % (alternating A/B); A/B builds: 2
+#define MPCQP_RSQ_NR 1
 #endif
 __device__ __forceinline__ double rsqrt_nr(double a) {
     double y = __builtin_amdgcn_rsq(a);
