@@ -409,7 +409,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             }
             r = (ln < q) ? a0 + a1 : 0.0;
             const double rmax = wave_max(fabs(r));
-            if (ln < q && r > kRTol * rmax) { t1 = u / r; kslot = ln; }
+            if (ln < q && r > kRTol * rmax) { t1 = fdiv(u, r); kslot = ln; }
             wave_argmin(t1, kslot);
         }
         if (!MPCQP_REG_RINV && q > 0) {
@@ -441,11 +441,11 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                 for (int t = 0; t < 4; ++t) cc[t] = nc[t];
             }
             const double rmax = wave_max(ln < q ? fabs(r) : 0.0);
-            if (ln < q && r > kRTol * rmax) { t1 = u / r; kslot = ln; }
+            if (ln < q && r > kRTol * rmax) { t1 = fdiv(u, r); kslot = ln; }
             wave_argmin(t1, kslot);
         }
         const bool dep = !(zn > kDepTol * dd);
-        const double t2 = dep ? INFINITY : -sp / zn;
+        const double t2 = dep ? INFINITY : fdiv(-sp, zn);
         const double t = t1 < t2 ? t1 : t2;
         if (isinf(t)) { status = ST_INFEASIBLE; break; }
         MPCQP_SUB(tsub, 2);
@@ -470,15 +470,15 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             if (zq > 0.0) {  // otherwise d2 = d_q e_q: no reflection, r_qq = d_q
                 const double nrm = sqrt(zn);
                 rqq = nrm;
-                vq = dq > 0.0 ? -zq / (dq + nrm) : dq - nrm;
-                beta = 2.0 / (vq * vq + zq);
+                vq = dq > 0.0 ? fdiv(-zq, dq + nrm) : dq - nrm;
+                beta = fdiv(2.0, vq * vq + zq);
             }
             wave_sync();
             if (ln == q) colb[q] = vq;
             if (MPCQP_REG_RINV) {
                 // R^-1 of [[R, d1], [0, r_qq]]: column q = (-R^-1 d1 / r_qq, 1 / r_qq), and
                 // R^-1 d1 is this pass's r
-                const double irq = 1.0 / rqq;
+                const double irq = fdiv(1.0, rqq);
                 if (ln < q) L.R[lrow(q) + ln] = -r * irq;
                 if (ln == q) { L.R[lrow(q) + q] = irq; act = p; }
             } else {
@@ -515,7 +515,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                 double hp = wave_prev(H);
                 pin(hp);
                 if (ln < NF) {
-                    const double ih = 1.0 / H;
+                    const double ih = fdiv(1.0, H);
                     rot[2 * ln] = on ? rb * ih : 1.0;
                     rot[2 * ln + 1] = on ? -(ln == k ? ra0 : hp) * ih : 0.0;
                 }
@@ -591,7 +591,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                     double n1 = r1;
                     if (bb != 0.0) {
                         const double hh = sqrt(a * a + bb * bb);
-                        const double ih = 1.0 / hh;
+                        const double ih = fdiv(1.0, hh);
                         const double c = a * ih, s_ = bb * ih;
                         n1 = -s_ * r0 + c * r1;
                         if (l < q) {

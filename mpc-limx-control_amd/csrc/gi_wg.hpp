@@ -681,9 +681,9 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             const double rmax = wave_max(fmax(ln < q ? fabs(r0) : 0.0, ln + 64 < q ? fabs(r1) : 0.0));
             double t1 = INFINITY;
             int ks = 0x7fffffff;
-            if (ln < q && r0 > kRTol * rmax) { t1 = us[ln] / r0; ks = ln; }
+            if (ln < q && r0 > kRTol * rmax) { t1 = fdiv(us[ln], r0); ks = ln; }
             if (TWO && ln + 64 < q && r1 > kRTol * rmax) {
-                const double tt = us[ln + 64] / r1;
+                const double tt = fdiv(us[ln + 64], r1);
                 if (tt < t1) { t1 = tt; ks = ln + 64; }
             }
             wave_argmin(t1, ks);
@@ -704,9 +704,9 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             r0 = (ln < q) ? v0 : 0.0;
             r1 = (TWO && ln + 64 < q) ? v1 : 0.0;
             const double rmax = wave_max(fmax(fabs(r0), fabs(r1)));
-            if (ln < q && r0 > kRTol * rmax) { t1 = us0 / r0; kslot = ln; }
+            if (ln < q && r0 > kRTol * rmax) { t1 = fdiv(us0, r0); kslot = ln; }
             if (TWO && ln + 64 < q && r1 > kRTol * rmax) {
-                const double tt = us1 / r1;
+                const double tt = fdiv(us1, r1);
                 if (tt < t1) { t1 = tt; kslot = ln + 64; }
             }
             wave_argmin(t1, kslot);
@@ -720,7 +720,7 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
         const double zn = NWH == 2 ? red[9] + red[12] : red[9];
         const double zq = NWH == 2 ? red[10] + red[13] : red[10];
         const bool dep = !(zn > kDepTol * dd);
-        const double t2 = dep ? INFINITY : -sp / zn;
+        const double t2 = dep ? INFINITY : fdiv(-sp, zn);
         const double t = t1 < t2 ? t1 : t2;
         if (isinf(t)) { status = ST_INFEASIBLE; break; }
         if (!isinf(t2)) {
@@ -753,14 +753,14 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             if (zq > 0.0) {
                 const double nrm = sqrt(zn);
                 rqq = nrm;
-                vq = dq > 0.0 ? -zq / (dq + nrm) : dq - nrm;
-                beta = 2.0 / (vq * vq + zq);
+                vq = dq > 0.0 ? fdiv(-zq, dq + nrm) : dq - nrm;
+                beta = fdiv(2.0, vq * vq + zq);
             }
             if (wv == 0) {
                 if (MPCQP_WG_RINV) {
                     // R^-1 of [[R, d1], [0, rqq]]: new column q = (-R^-1 d1 / rqq, 1 / rqq), and
                     // R^-1 d1 is this pass's r (wave 0's r0 / r1)
-                    const double irq = 1.0 / rqq;
+                    const double irq = fdiv(1.0, rqq);
                     if (ln < q) Lc[lrow(q) + ln] = -r0 * irq;
                     if (TWO && ln + 64 < q) Lc[lrow(q) + ln + 64] = -r1 * irq;
                     if (ln == 0) {
@@ -773,7 +773,7 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
                     if (TWO && ln + 64 < q) Lc[roff(q) + ln + 64] = dB[ln + 64];
                     if (ln == 0) {
                         Lc[roff(q) + q] = rqq;
-                        rinv[q] = 1.0 / rqq;
+                        rinv[q] = fdiv(1.0, rqq);
                         acts[q] = p;
                         L.st[p] = 2;
                     }
@@ -818,7 +818,7 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
                     if (j0 < NF) {
                         const bool on = j0 >= k && j0 < qn;
                         const double pv = (j0 == k) ? ra0 : hp0;
-                        const double ih = 1.0 / H0;
+                        const double ih = fdiv(1.0, H0);
                         rot[2 * j0] = on ? rb0 * ih : 1.0;
                         rot[2 * j0 + 1] = on ? -pv * ih : 0.0;
                     }

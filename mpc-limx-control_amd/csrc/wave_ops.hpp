@@ -230,6 +230,24 @@ __device__ __forceinline__ double rsqrt_nr(double a) {
     return y;
 }
 
+// a / b for the dual loops' step lengths, reflector and rotation scalings: the IEEE division
+// (~12 VALU: v_div_scale x2, v_rcp, five FMAs, v_div_fmas, v_div_fixup) or, with
+// MPCQP_FAST_DIV, a * (1 / b) from v_rcp_f64 and two Newton steps (5 VALU; within ~2 ulp; every
+// divisor there is positive and normal)
+#ifndef MPCQP_FAST_DIV
+#define MPCQP_FAST_DIV 0
+#endif
+__device__ __forceinline__ double fdiv(double a, double b) {
+    if constexpr (MPCQP_FAST_DIV) {
+        double y = __builtin_amdgcn_rcp(b);
+        y = fma(y, fma(-b, y, 1.0), y);
+        y = fma(y, fma(-b, y, 1.0), y);
+        return a * y;
+    } else {
+        return a / b;
+    }
+}
+
 // Materialise v in a VGPR at this point: arithmetic producing v cannot sink past it.
 __device__ __forceinline__ void pin(double &v) { asm volatile("" : "+v"(v)); }
 
