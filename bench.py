@@ -415,10 +415,10 @@ def launch_ranks(args, argv):
 
 
 def shard(total_states, world, rank):
-    """contiguous range of whole states for `rank` -> (first state, number of states)"""
-    base, rem = divmod(total_states, world)
-    s0 = rank * base + min(rank, rem)
-    return s0, base + (1 if rank < rem else 0)
+    """contiguous range of whole states for `rank` -> (first state, number of states): the
+    library's mpcqp_shard, the arithmetic its multi-GPU group uses"""
+    from mpcqp.group import shard as lib_shard
+    return lib_shard(total_states, world, rank)
 
 
 def slice_batch(batch, i0, n):
@@ -459,6 +459,10 @@ def main():
     ap.add_argument("--selection-dry-run", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--select", choices=("fused", "separate"), default="fused",
                     help="selection record from the solve kernels (fused) or k_select_min")
+    ap.add_argument("--capi-group", action="store_true",
+                    help="drive the step through the library's multi-GPU group (include/mpcqp.h "
+                         "mpcqp_group_*: its own RCCL communicator, one all-gather per step); "
+                         "torch.distributed only hands rank 0's RCCL id to the other ranks")
     ap.add_argument("--serial-select", action="store_true",
                     help="N > 1: wait for each step's all-gather before the next solve (default: "
                          "the collective of step s overlaps the solve of step s + 1)")
@@ -514,6 +518,14 @@ def main():
     else:
         formed = dict(backend=None, world_size=1, ranks=[me])
 
+    group = None
+    if args.capi_group and not dry:
+        from mpcqp.group import Group, unique_id
+        uid = [unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        group = Group(p, rank=(local, world, rank, uid[0]))
+
     def run_line(batch_local, index_base, steps, warmup, serial=False):
         """time `steps` steps of solve + selection on this rank's shard; returns
         (elapsed max over ranks, kernel ms, select ms, best record, status, iters, eng).
@@ -532,6 +544,15 @@ def main():
 
             def solve_into(rec):
                 rec.copy_(torch.from_numpy(host_record(cost, status, U, index_base)))
+        elif group is not None:
+            # the C-ABI group (csrc/group.hip): solve + the library's own RCCL all-gather of the
+            # records + the device reduction, pipelined inside the library
+            from mpcqp.engine import BatchEngine
+            eng = BatchEngine.wrap(p, group.ctx(0), local)
+            d = eng.upload(batch_local)
+            torch.cuda.synchronize()
+            shard_io = [dict(d, base=index_base)]
+            best = torch.zeros(1 + nV, dtype=torch.int64, device=dev)
         else:
             from mpcqp.engine import BatchEngine
             eng = BatchEngine(p, device=local)
@@ -544,9 +565,13 @@ def main():
                 else:
                     eng.solve(d)
                     eng.select_record(d, rec, index_base=index_base)
-        pipe = PipelinedSelect(dist, recs, gathered, best, reduce) if world > 1 else None
+        pipe = PipelinedSelect(dist, recs, gathered, best, reduce) \
+            if world > 1 and group is None else None
 
         def step():
+            if group is not None:
+                group.solve_select(shard_io, [best])
+                return
             if pipe is None:  # world == 1: best is recs[0]
                 solve_into(recs[0])
                 return
@@ -556,6 +581,8 @@ def main():
                 pipe.drain()
 
         def sync():
+            if group is not None:
+                group.sync()
             if pipe is not None:
                 pipe.drain()
             if not dry:
@@ -583,7 +610,24 @@ def main():
             elapsed = float(t.item())
         mpc_ms = sel_ms = None
         kern = {}
-        if not dry:
+        if group is not None:
+            # the library's events around each solve call (slot 1) and kernel (2: the one-wave
+            # kernel, 3: the overflow launch), a pass of `steps` more steps after the timed ones
+            eng.enable_timing(True)
+            for _ in range(steps):
+                step()
+            sync()
+            for w, name in ((2, eng.fused_kernel), (3, "k_mpc_wg")):
+                ms, n = eng.kernel_ms_sum(w)
+                if n:
+                    kern[name] = dict(ms=ms / n, launches=n)
+            ms, n = eng.kernel_ms_sum(1)
+            mpc_ms = ms / max(1, n)
+            sel_ms = 0.0
+            eng.enable_timing(False)
+            status = d["status"].cpu().numpy()
+            iters = d["iters"].cpu().numpy()
+        elif not dry:
             # solve and selection durations: torch events around the calls, a separate pass of
             # `steps` more steps after the timed ones
             stream = torch.cuda.current_stream()
@@ -654,7 +698,7 @@ def main():
     # N > 1: the same steps with each all-gather waited for before the next solve (reported
     # beside the overlapped value, never as it)
     serial_ms = None
-    if world > 1 and not args.serial_select:
+    if world > 1 and not args.serial_select and group is None:
         el_s, *rest = run_line(local_batch, i0, args.steps, args.warmup, serial=True)
         if rest[5] is not None:
             rest[5].close()
@@ -694,6 +738,12 @@ def main():
                               (" + one all-gather of [key | U] records + k_reduce_records"
                                if world > 1 else " (single GPU)")),
                    selected=dict(index=bidx, cost=bcost))
+        if group is not None:
+            cfg["selection"] = ("C-ABI group (mpcqp_group_solve_select, csrc/group.hip): fused "
+                                "record + ncclAllGather from libmpcqp.so's own communicator + "
+                                "k_reduce_records, the collective of step s beside the solve of "
+                                "step s + 1")
+            cfg["capi_group"] = True
         if world > 1:
             cfg["selection_overlap"] = (
                 "serial: each all-gather waited for before the next solve" if args.serial_select
@@ -782,6 +832,8 @@ def main():
         print(json.dumps(out), flush=True)
     elif eng is not None:
         eng.close()
+    if group is not None:
+        group.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

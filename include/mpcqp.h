@@ -54,6 +54,9 @@
  * mpcqp_ctx_reserve               (new) pre-sizes the context's buffers (no allocation per tick)
  * mpcqp_kf_update                 stateEstimator::update (include/stateEstimator.h:217-337),
  *                                 batched
+ * mpcqp_group_*, mpcqp_shard      (new) the batch over the GPUs of a node with one RCCL
+ *                                 all-gather per step, for the C++ control loop
+ *                                 (src/mpc_control_fake_state.cpp:108-149)
  */
 #ifndef MPCQP_H
 #define MPCQP_H
@@ -242,6 +245,64 @@ int mpcqp_reduce_records(mpcqp_ctx *ctx, int n, const int64_t *records, int64_t 
 int mpcqp_batch_solve_select(mpcqp_ctx *ctx, int B, const double *x0, const double *xref,
                              const double *lin, const uint64_t *contact, double *U, double *cost,
                              int *status, int *iters, int64_t index_base, int64_t *record);
+
+/* ---- multi-GPU group: the batch sharded over devices, ONE RCCL collective per step --------
+ * SURVEY.md 8b ("ownership": a context that owns the communicator) and 8e; the C++ caller is
+ * the control loop of src/mpc_control_fake_state.cpp:108-149 (MPC::run ->
+ * computeSupportFootForce, include/MPCController.h:183-196) at batch scale.  A group holds one
+ * context per device it drives and an RCCL communicator over all ranks (xGMI between the GPUs
+ * of one node).  Each step: every rank solves its shard -- contiguous whole states of C gait
+ * candidates, mpcqp_shard -- with mpcqp_batch_solve_select, the ranks exchange the [key | U]
+ * selection records with ONE ncclAllGather, and every rank reduces them on device
+ * (mpcqp_reduce_records): the global minimum-cost instance (fp32 cost, lowest global index on
+ * ties), on every rank, with no host synchronisation inside the step. */
+#define MPCQP_GROUP_UID_BYTES 128
+typedef struct mpcqp_group mpcqp_group;
+/* contiguous shard of whole states for `rank` of `nranks` (host arithmetic, no device): the
+ * first `total_states % nranks` ranks take one state more.  bench.py and mpcqp/dist.py use it. */
+int mpcqp_shard(int total_states, int nranks, int rank, int *first_state, int *states);
+/* one process driving `ndev` devices (ncclCommInitAll): ranks 0..ndev-1 = devices[0..ndev-1] */
+int mpcqp_group_create(const mpcqp_model *model, int ndev, const int *devices, mpcqp_group **out);
+/* one process per device (torchrun / MPI style): rank `rank` of `nranks` on `device`.  uid
+ * (MPCQP_GROUP_UID_BYTES) comes from mpcqp_group_unique_id on one rank and is handed to every
+ * rank by the caller's own channel; every rank must call this (it blocks until all have). */
+int mpcqp_group_unique_id(unsigned char *uid);
+int mpcqp_group_create_rank(const mpcqp_model *model, int device, int nranks, int rank,
+                            const unsigned char *uid, mpcqp_group **out);
+int mpcqp_group_destroy(mpcqp_group *g);
+/* *local: devices this process drives; *nranks: ranks of the communicator; *first_rank: the rank
+ * of local member 0 (local member i is rank first_rank + i) */
+int mpcqp_group_info(const mpcqp_group *g, int *local, int *nranks, int *first_rank);
+/* local member i's context (its device, stream and buffers; e.g. mpcqp_ctx_reserve, timing) */
+mpcqp_ctx *mpcqp_group_ctx(mpcqp_group *g, int i);
+/* One step on device pointers.  Per local member i (device of member i):
+ *   B[i] instances with global index base[i] (x0 / xref / lin / contact / U / cost / status /
+ *   iters as for mpcqp_batch_solve, pointer arrays indexed by member), best[i] [1 + nu*N] int64
+ *   receives the global record (key, winner's U) -- the same on every rank.
+ * Asynchronous: the solve runs on the member's context stream, the all-gather and the reduction
+ * on the group's collective stream of that device, so this step's collective overlaps the next
+ * step's solve.  best[i] is complete after mpcqp_group_sync, or, for work enqueued afterwards on
+ * the member's context stream, after mpcqp_group_wait.  Records alternate between two buffers:
+ * a step's solve waits (on device) for the all-gather two steps back, nothing else. */
+int mpcqp_group_solve_select(mpcqp_group *g, const int *B, const int64_t *base,
+                             const double *const *x0, const double *const *xref,
+                             const double *const *lin, const uint64_t *const *contact,
+                             double *const *U, double *const *cost, int *const *status,
+                             int *const *iters, int64_t *const *best);
+/* make each member's context stream wait (on device) for its collective stream: results of the
+ * steps issued so far are visible to work enqueued on the context streams afterwards */
+int mpcqp_group_wait(mpcqp_group *g);
+/* wait on the host for every member's streams */
+int mpcqp_group_sync(mpcqp_group *g);
+/* Host-pointer form for a single-process group (mpcqp_group_create; every rank local): the global
+ * batch of S states x C candidates (host arrays, the layouts of mpcqp_batch_solve) is split with
+ * mpcqp_shard, staged through pinned buffers the group owns, solved and selected as above;
+ * U / cost / status / iters come back for the whole batch and best_host [1 + nu*N] receives the
+ * global record.  Synchronous. */
+int mpcqp_group_solve_select_host(mpcqp_group *g, int S, int C, const double *x0,
+                                  const double *xref, const double *lin, const uint64_t *contact,
+                                  double *U, double *cost, int *status, int *iters,
+                                  int64_t *best_host);
 
 /* ---- device-generated inputs, per-state selection and the closed loop ---- *
  * SRBM fast-path contexts only.  S states x C gait candidates, instance b = s*C + c.

@@ -50,6 +50,11 @@ namespace mpcqp {
 #ifndef MPCQP_CHOL_PF
 #define MPCQP_CHOL_PF 4
 #endif
+// Cholesky and J = L^-T folded into one register row per lane (see the sweep); 0 keeps the
+// fused two-array sweep (A/B builds)
+#ifndef MPCQP_PAIR_FOLD
+#define MPCQP_PAIR_FOLD 1
+#endif
 // the dual loop keeps R^-1 instead of R (r = R^-1 d as a lane-parallel product, no serial
 // back substitution); 0 keeps R (A/B builds)
 #ifndef MPCQP_PAIR_RINV
@@ -180,6 +185,79 @@ __device__ __forceinline__ int pair_sorted_instance(const MpcArgs &a) {
     const unsigned m1 = (unsigned)(__ballot(ln < 16 && c < gn && rank == r0 + 1) & 0xffffull);
     const unsigned m = ln >= kHalf ? m1 : m0;
     return m ? g0 + __builtin_ctz(m) : a.B;  // a.B: no instance (rank beyond a short group)
+}
+
+// ---- the folded sweep's trailing update (see pair_mpc): slot J of every lane -= the column's
+// entry of row J, broadcast in the FMA itself (v_fmac_f64_dpp row_newbcast: lane J & 15 of each
+// 16-lane row, from the row copy A -- lanes 0-15 of the half -- or B -- lanes 16-31 -- of
+// row_pair), times the lane's own multiplier m.  Columns k (A0/B0, m0) and k + 1 (A1/B1, m1).
+// The compiler does not form DPP FMAs itself (its VOP3 v_fma_f64 has no DPP); "s_nop 1" gives
+// the DPP source its two wait states after the VALU that wrote it.
+template <int J>
+__device__ __forceinline__ void fold_dpp4(double &s0, double &s1, double &s2, double &s3,
+                                          double A0, double B0, double m0, double A1, double B1,
+                                          double m1) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, -%4, %12 row_newbcast:%c14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, -%5, %12 row_newbcast:%c15 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, -%6, %12 row_newbcast:%c16 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, -%7, %12 row_newbcast:%c17 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, -%8, %13 row_newbcast:%c14 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, -%9, %13 row_newbcast:%c15 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %2, -%10, %13 row_newbcast:%c16 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %3, -%11, %13 row_newbcast:%c17 row_mask:0xf bank_mask:0xf"
+        : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3)
+        : "v"(J < 16 ? A0 : B0), "v"(J + 1 < 16 ? A0 : B0), "v"(J + 2 < 16 ? A0 : B0),
+          "v"(J + 3 < 16 ? A0 : B0), "v"(J < 16 ? A1 : B1), "v"(J + 1 < 16 ? A1 : B1),
+          "v"(J + 2 < 16 ? A1 : B1), "v"(J + 3 < 16 ? A1 : B1), "v"(m0), "v"(m1),
+          "i"(J & 15), "i"((J + 1) & 15), "i"((J + 2) & 15), "i"((J + 3) & 15));
+}
+template <int J>
+__device__ __forceinline__ void fold_dpp2(double &s0, double &s1, double A0, double B0, double m0,
+                                          double A1, double B1, double m1) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, -%2, %6 row_newbcast:%c8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, -%3, %6 row_newbcast:%c9 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %0, -%4, %7 row_newbcast:%c8 row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f64_dpp %1, -%5, %7 row_newbcast:%c9 row_mask:0xf bank_mask:0xf"
+        : "+v"(s0), "+v"(s1)
+        : "v"(J < 16 ? A0 : B0), "v"(J + 1 < 16 ? A0 : B0), "v"(J < 16 ? A1 : B1),
+          "v"(J + 1 < 16 ? A1 : B1), "v"(m0), "v"(m1), "i"(J & 15), "i"((J + 1) & 15));
+}
+// one slot, one column (the in-panel update of column k + 1 by column k)
+template <int J>
+__device__ __forceinline__ void fold_dpp1(double &s, double A, double B, double m) {
+    asm("s_nop 1\n\t"
+        "v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%c3 row_mask:0xf bank_mask:0xf"
+        : "+v"(s)
+        : "v"(J < 16 ? A : B), "v"(m), "i"(J & 15));
+}
+// the trailing update of slots k + 2 .. NF - 1 for the column pair (k, k + 1)
+template <int NF, int K, int J = K + 2>
+__device__ __forceinline__ void fold_trailing(double (&s)[NF], double A0, double B0, double m0,
+                                              double A1, double B1, double m1) {
+    if constexpr (J + 3 < NF) {
+        fold_dpp4<J>(s[J], s[J + 1], s[J + 2], s[J + 3], A0, B0, m0, A1, B1, m1);
+        fold_trailing<NF, K, J + 4>(s, A0, B0, m0, A1, B1, m1);
+    } else if constexpr (J + 1 < NF) {
+        fold_dpp2<J>(s[J], s[J + 1], A0, B0, m0, A1, B1, m1);
+        fold_trailing<NF, K, J + 2>(s, A0, B0, m0, A1, B1, m1);
+    }
+}
+template <int NF, int K = 0>
+__device__ __forceinline__ void fold_in_panel(double (&s)[NF], double A, double B, double m, int k) {
+    if constexpr (K + 1 < NF) {
+        if (k == K) fold_dpp1<K + 1>(s[K + 1], A, B, m);
+        else fold_in_panel<NF, K + 2>(s, A, B, m, k);
+    }
+}
+template <int NF, int K = 0>
+__device__ __forceinline__ void fold_trailing_k(double (&s)[NF], int k, double A0, double B0,
+                                                double m0, double A1, double B1, double m1) {
+    if constexpr (K + 2 < NF) {
+        if (k == K) fold_trailing<NF, K>(s, A0, B0, m0, A1, B1, m1);
+        else fold_trailing_k<NF, K + 2>(s, k, A0, B0, m0, A1, B1, m1);
+    }
 }
 
 template <int NU, int N, int MODEL, bool GEN>
@@ -541,10 +619,12 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 for (int q = 0; q <= hl; ++q) Hb[lrow(hl) + q] = (q == hl) ? 1.0 : 0.0;
         }
         wave_sync();
+#if !MPCQP_PAIR_FOLD
         double h[NF];
     #pragma unroll
         for (int q = 0; q < NF; ++q) h[q] = Hb[lrow(hl) + q];
         wave_sync();
+#endif
         MPCQP_STAMP(a.stamps, 3, tst);
         MPCQP_CUT(a.cut, 3);
 
@@ -560,6 +640,95 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         const bool any_ok = __ballot(ok) != 0ull;
         bool ok2 = ok;
         if (any_ok) {
+#if MPCQP_PAIR_FOLD
+            // ---- Cholesky and the inverse sweep FOLDED into one register row per lane.  Lane l owns
+            //      row l of the symmetric H_FF, whole (slots q > l read from the packed lower
+            //      triangle's column l).  Right-looking, lane l is an ordinary Cholesky row for its
+            //      slots q <= l: at step k its slot k becomes L(l, k), the multiplier of its trailing
+            //      update s_j -= L(l, k) L(j, k).  Its slots q > l hold the J part: every step k < l
+            //      applies the same update to them (the instruction is uniform), so after step l - 1
+            //      they hold exactly the Schur-complement entries H'(j, l) -- the values lane j holds
+            //      in its slot l, computed by the same FMAs in the same order -- i.e. L(j, l) L(l, l).
+            //      Lane l sits out the trailing update of step l itself, and its own slot l is
+            //      negated after the scaling (-L(l, l)): from then on [-L(l,l), H'(l+1.., l)] is
+            //      -piv_l times [ik_l, -L(l+1.., l) ik_l], the forward substitution L y = e_l after its
+            //      step l, and the later steps k > l (in which lane l takes part with its slot k as
+            //      the multiplier y_k) finish it.  At the end slots q >= l are scaled by -1 / piv_l
+            //      (row l of J = L^-T) and slots q < l (its row of L, dead) zeroed.  Lane 31 of each
+            //      half carries g as row 31 of the padded matrix (below every row: a plain Cholesky
+            //      row throughout) and ends with t = L^-1 g.  One FMA per (step, slot) instead of the
+            //      fused sweep's two (one for H, one for J); the two triangles of the square the lanes
+            //      swept are one triangle each, and the J array costs no registers of its own.
+            static_assert(Lay::oRow == Lay::oR + lrow(kHalf - 1), "row 31 (g) is the row buffer");
+            if (hl < NF) rowbuf[hl] = gv;
+            wave_sync();
+            {
+                const double *Hr = D + Lay::oR + lrow(hl), *Hc = D + Lay::oR + hl;
+    #pragma unroll
+                for (int q = 0; q < NF; ++q) {
+                    const double lo_ = Hr[q], up_ = Hc[lrow(q)];  // (q, l) read for q > l
+                    Jr[q] = (q <= hl) ? lo_ : up_;
+                }
+            }
+            wave_sync();
+            static_assert(MPCQP_CHOL_CB == 2, "the folded sweep runs column pairs");
+            double *dg = rot;  // pivot of every column (uniform stores), for the final scaling
+            double piv = hbcast<0>(Jr[0]);
+            bool bad = !(piv > 0.0);
+            double ik = rsqrt_nr(piv);
+    #pragma unroll
+            for (int k = 0; k < NF; k += 2) {
+                const double pk = piv;
+                // column k: lanes > k get L(l, k), lanes < k their J entry y_k; lane k L(k, k),
+                // negated (its J part's first entry), and multiplier 0 (it sits out step k)
+                Jr[k] *= ik;
+                const bool own0 = hl == k;
+                const double m0 = own0 ? 0.0 : Jr[k];
+                Jr[k] = own0 ? -Jr[k] : Jr[k];
+                double A0, B0;
+                row_pair(m0, A0, B0);  // the column's rows 0-15 / 16-31 in every row of the half
+                fold_in_panel<NF>(Jr, A0, B0, m0, k);  // slot k + 1 -= L(k + 1, k) m0
+                const double pc = hbcast(Jr[k + 1], k + 1);
+                bad |= !(pc > 0.0);
+                const double ik1 = rsqrt_nr(pc);
+                Jr[k + 1] *= ik1;
+                const bool own1 = hl == k + 1;
+                const double m1 = own1 ? 0.0 : Jr[k + 1];
+                Jr[k + 1] = own1 ? -Jr[k + 1] : Jr[k + 1];
+                double A1, B1;
+                row_pair(m1, A1, B1);
+                double pivn = 1.0, ikn = 1.0;
+                if (k + 2 < NF) {  // next pivot ahead of the trailing update (on lane k + 2)
+                    double hn = Jr[k + 2 < NF ? k + 2 : k];
+                    hn -= Jr[k] * Jr[k];
+                    pivn = hbcast(hn - Jr[k + 1] * Jr[k + 1], k + 2);
+                    bad |= !(pivn > 0.0);
+                    ikn = rsqrt_nr(pivn);
+                }
+                dg[k] = pk;
+                dg[k + 1] = pc;
+                // trailing update: slot j -= L(j, k) m0 + L(j, k + 1) m1, the L(j, .) broadcast by
+                // the FMA's own DPP (no LDS round trip)
+                fold_trailing_k<NF>(Jr, k, A0, B0, m0, A1, B1, m1);
+    #pragma unroll
+                for (int j = 0; j < NF; ++j)
+                    if (j >= k) pin(Jr[j]);
+                piv = pivn;
+                ik = ikn;
+                pin(piv);
+                pin(ik);
+                step_fence();
+            }
+            {   // rows of J: slots >= l times -1 / piv_l, the L row below zeroed; lane 31 keeps t
+                wave_sync();
+                const bool gl = hl == kHalf - 1;
+                const double pl = dg[hl < NF ? hl : 0];
+                const double cl = gl ? 1.0 : -1.0 / pl;
+                const int lim = gl ? 0 : (hl < NF ? hl : NF);
+    #pragma unroll
+                for (int j = 0; j < NF; ++j) Jr[j] = (j < lim) ? 0.0 : Jr[j] * cl;
+            }
+#else
             // ---- Cholesky fused with the inverse sweep.  Right-looking, lane l owns row l of H_FF
             //      (identity padding beyond nf).  Step k's column of L, broadcast from LDS for the
             //      trailing update, is also the operand of step k of the forward substitution
@@ -652,6 +821,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 pin(ik);
                 step_fence();
             }
+#endif
             if (ok && bad) status = ST_NOT_PD;
             ok2 = ok && status == ST_OK;
             MPCQP_STAMP(a.stamps, 5, tst);

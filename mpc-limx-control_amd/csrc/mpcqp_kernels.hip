@@ -1874,4 +1874,17 @@ int mpcqp_reduce_records(mpcqp_ctx *c, int n, const int64_t *records, int64_t *b
     return hip_status(hipGetLastError());
 }
 
+// (library-internal, group.hip) the same reduction on another stream of the context's device:
+// the multi-GPU group runs it on its collective stream, after the all-gather
+__attribute__((visibility("hidden"))) int mpcqp_reduce_records_on(mpcqp_ctx *c, void *stream, int n,
+                                                                  const int64_t *records,
+                                                                  int64_t *best) {
+    if (!c || !records || !best || n <= 0) return MPCQP_ERR_BAD_ARG;
+    hipSetDevice(c->device);
+    hipLaunchKernelGGL(k_reduce_records, dim3(1), dim3(64), 0, (hipStream_t)stream, n,
+                       c->m.nu * c->m.N, reinterpret_cast<const long long *>(records),
+                       reinterpret_cast<long long *>(best));
+    return hip_status(hipGetLastError());
+}
+
 }  // extern "C"

@@ -163,4 +163,57 @@ class ConvexMpc {
     std::vector<int> iters_;
 };
 
+// The batch of S states x C gait candidates over several GPUs of one node, from one controller
+// process: mpcqp_group (one context per device, the library's RCCL communicator, ONE all-gather
+// of the selection records per tick).  The choice is the global minimum (fp32 cost, lowest
+// global index), the same rule as ConvexMpc::solve_batch and the multi-process path.
+class GroupMpc {
+  public:
+    GroupMpc(const ModelSpec &spec, const std::vector<int> &devices) : spec_(spec) {
+        int rc = mpcqp_group_create(&spec_.m, (int)devices.size(), devices.data(), &g_);
+        if (rc != MPCQP_OK) throw std::runtime_error(std::string("mpcqp_group_create: ") + mpcqp_status_string(rc));
+    }
+    ~GroupMpc() { if (g_) mpcqp_group_destroy(g_); }
+    GroupMpc(const GroupMpc &) = delete;
+    GroupMpc &operator=(const GroupMpc &) = delete;
+
+    mpcqp_group *group() { return g_; }
+
+    // S states x C candidates (host arrays, the mpcqp.h instance-major layout, instance s*C + c)
+    MpcChoice solve_batch(const double *x0, const double *xref, const double *lin,
+                          const uint64_t *contacts, int S, int C) {
+        const int nv = spec_.m.nu * spec_.m.N;
+        const size_t B = (size_t)S * C;
+        U_.resize(B * nv);
+        cost_.resize(B);
+        iters_.resize(B);
+        rec_.resize(1 + (size_t)nv);
+        MpcChoice out;
+        out.status.resize(B);
+        int rc = mpcqp_group_solve_select_host(g_, S, C, x0, xref, lin, contacts, U_.data(),
+                                               cost_.data(), out.status.data(), iters_.data(),
+                                               rec_.data());
+        if (rc != MPCQP_OK) throw std::runtime_error(std::string("mpcqp_group_solve_select_host: ") + mpcqp_status_string(rc));
+        if (rec_[0] != INT64_MAX) {
+            out.index = (int)(rec_[0] & 0x7fffffff);
+            out.cost = cost_[(size_t)out.index];
+            out.U.resize((size_t)nv);
+            std::memcpy(out.U.data(), &rec_[1], sizeof(double) * nv);  // the record's U bits
+        }
+        return out;
+    }
+
+    const std::vector<double> &all_U() const { return U_; }
+    const std::vector<double> &all_cost() const { return cost_; }
+    const std::vector<int> &all_iters() const { return iters_; }
+    const std::vector<int64_t> &record() const { return rec_; }
+
+  private:
+    ModelSpec spec_;
+    mpcqp_group *g_ = nullptr;
+    std::vector<double> U_, cost_;
+    std::vector<int> iters_;
+    std::vector<int64_t> rec_;
+};
+
 }  // namespace mpcqp

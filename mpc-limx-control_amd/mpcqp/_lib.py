@@ -32,6 +32,9 @@ EXPORTS = [
     "mpcqp_batch_solve_gait", "mpcqp_batch_select_state", "mpcqp_batch_plant_srbm",
     "mpcqp_rollout", "mpcqp_fk_feet", "mpcqp_kf_update", "mpcqp_ctx_reserve",
     "mpcqp_ctx_fk_feet_host", "mpcqp_set_warm_start",
+    "mpcqp_shard", "mpcqp_group_create", "mpcqp_group_unique_id", "mpcqp_group_create_rank",
+    "mpcqp_group_destroy", "mpcqp_group_info", "mpcqp_group_ctx", "mpcqp_group_solve_select",
+    "mpcqp_group_wait", "mpcqp_group_sync", "mpcqp_group_solve_select_host",
     "mpcqp_status_string", "mpcqp_device_count", "mpcqp_build_id",
 ]
 
@@ -105,6 +108,19 @@ def lib():
     L.mpcqp_last_kernel_ms.restype = C.c_double
     L.mpcqp_kernel_ms_sum.argtypes = [vp, i, C.POINTER(C.c_int)]
     L.mpcqp_kernel_ms_sum.restype = C.c_double
+    if hasattr(L, "mpcqp_group_create"):  # absent from A/B builds of older sources
+        L.mpcqp_shard.argtypes = [i, i, i, vp, vp]
+        L.mpcqp_group_create.argtypes = [C.POINTER(Model), i, vp, C.POINTER(vp)]
+        L.mpcqp_group_unique_id.argtypes = [vp]
+        L.mpcqp_group_create_rank.argtypes = [C.POINTER(Model), i, i, i, vp, C.POINTER(vp)]
+        L.mpcqp_group_destroy.argtypes = [vp]
+        L.mpcqp_group_info.argtypes = [vp, vp, vp, vp]
+        L.mpcqp_group_ctx.argtypes = [vp, i]
+        L.mpcqp_group_ctx.restype = vp
+        L.mpcqp_group_solve_select.argtypes = [vp] * 12
+        L.mpcqp_group_wait.argtypes = [vp]
+        L.mpcqp_group_sync.argtypes = [vp]
+        L.mpcqp_group_solve_select_host.argtypes = [vp, i, i] + [vp] * 9
     L.mpcqp_status_string.argtypes = [i]
     L.mpcqp_status_string.restype = C.c_char_p
     L.mpcqp_build_id.argtypes = []

@@ -33,13 +33,25 @@ class BatchEngine:
         check("mpcqp_ctx_create", lib().mpcqp_ctx_create(C.byref(m), device, C.byref(ctx)))
         del keep
         self.ctx = ctx
+        self.own = True
         if stream is None:  # share torch's stream so uploads/memsets are ordered before us
             stream = torch.cuda.current_stream(device).cuda_stream
         check("mpcqp_set_stream", lib().mpcqp_set_stream(self.ctx, C.c_void_p(stream)))
 
+    @classmethod
+    def wrap(cls, params: dict, ctx, device: int = 0):
+        """an engine over a context someone else owns (a member of mpcqp.group.Group: its
+        stream stays the group's; close() leaves the context alone)"""
+        import torch
+        e = cls.__new__(cls)
+        e.torch, e.p, e.device, e.nV = torch, params, device, params["nu"] * params["N"]
+        e.ctx, e.own = ctx, False
+        return e
+
     def close(self):
         if self.ctx:
-            lib().mpcqp_ctx_destroy(self.ctx)
+            if self.own:
+                lib().mpcqp_ctx_destroy(self.ctx)
             self.ctx = None
 
     def __del__(self):

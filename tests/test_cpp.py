@@ -20,12 +20,12 @@ SHIM = os.path.join(ROOT, "tests", "cpp", "eigen_shim")  # test-only Eigen / lim
 COMPAT = os.path.join(PKG, "compat")
 
 
-def _build(name, out_dir, src=None, extra=()):
+def _build(name, out_dir, src=None, extra=(), post=()):
     exe = os.path.join(str(out_dir), name)
     cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-Werror", *extra,
            "-I", SHIM, "-I", os.path.join(PKG, "include"),
            os.path.join(ROOT, "tests", "cpp", (src or name) + ".cpp"),
-           "-L", LIBDIR, "-lmpcqp", "-Wl,-rpath," + LIBDIR, "-Wl,-rpath,/opt/rocm/lib",
+           "-L", LIBDIR, "-lmpcqp", *post, "-Wl,-rpath," + LIBDIR, "-Wl,-rpath,/opt/rocm/lib",
            "-o", exe]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
@@ -41,6 +41,11 @@ def exes(tmp_path_factory):
     out["qp_test_eigen"] = _build("qp_test_eigen", d, extra=("-I", COMPAT))
     out["mpc_controller_compat"] = _build("mpc_controller_compat", d, src="mpc_controller",
                                           extra=("-DMPCQP_COMPAT_MPC", "-I", COMPAT))
+    # the multi-GPU group from C++ (mpcqp::GroupMpc); the harness's own reference run uses the
+    # HIP runtime API for its device buffers
+    out["group_test"] = _build("group_test", d, extra=("-D__HIP_PLATFORM_AMD__", "-I",
+                                                       "/opt/rocm/include"),
+                               post=("-L", "/opt/rocm/lib", "-lamdhip64"))
     return out
 
 
@@ -263,3 +268,25 @@ def test_compat_mpc_class_matches_basic_mpc(gpu, exes, tmp_path):
         outs.append(r.stdout)
     assert len(outs[0].strip().splitlines()) == T
     assert outs[0] == outs[1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gait", ["alternating", "mixed"])
+def test_cpp_group_matches_solve_select(gpu, exes, tmp_path, gait):
+    """mpcqp::GroupMpc (include/mpcqp/convex_mpc.hpp -> mpcqp_group_solve_select_host: the
+    library's RCCL communicator, one all-gather, the device reduction) on the box's device:
+    every per-instance output and the selection record bit-identical to one context's
+    mpcqp_batch_solve_select, over two ticks (both record buffers).  `mixed` routes instances
+    through the overflow kernel too."""
+    import mpcqp
+    p = mpcqp.model_params("B")
+    S, Cn = 37, 16
+    b = mpcqp.make_batch(p, S * Cn, seed=4242, gait=gait)
+    f = tmp_path / "in.bin"
+    with open(f, "wb") as fh:
+        for k in ("x0", "xref", "lin", "contact"):
+            fh.write(np.ascontiguousarray(b[k]).tobytes())
+    r = subprocess.run([exes["group_test"], str(S), str(Cn), str(f), "0"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "same_outputs 1 same_record 1" in r.stdout, r.stdout

@@ -14,7 +14,7 @@ for spec in "$@"; do
   flags="$flags -DMPCQP_VARIANT_TAG=\"$name-$(echo "$TU $flags" | sha1sum | cut -c1-8)\""
   ( mkdir -p "build/$name" && /opt/rocm/bin/hipcc $HF $flags -c -o "build/$name/$TU.o" csrc/$TU.hip && \
     /opt/rocm/bin/hipcc $HF -shared -o "lib/libmpcqp_$name.so" $(ls build/rel/*.o | grep -v $TU.o) \
-        "build/$name/$TU.o" && \
+        "build/$name/$TU.o" -L/opt/rocm/lib -lrccl && \
     echo "$name $(/opt/rocm/bin/hipcc $HF $flags -Rpass-analysis=kernel-resource-usage --cuda-device-only -c \
         -o "/tmp/ru_$name.o" csrc/$TU.hip 2>&1 | grep -E 'VGPRs Spill' | head -1 \
         | sed 's/.*remark://;s/\[-R.*//')" ) &
