@@ -103,6 +103,40 @@ __device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v,
 constexpr int kSelSlots = 256, kSelStride = 16, kSelTickets = 16;
 // key slots, then kSelTickets ticket words and the global ticket, each on its own 128 B
 constexpr int kSelWords = (kSelSlots + kSelTickets + 1) * kSelStride;
+// the finalizer: the minimum over the slots (and k0), the winner's U row into the record, slots
+// and tickets re-armed for the next call on the stream
+__device__ __forceinline__ void sel_final_reduce(const MpcArgs &a, int nV,
+                                                 unsigned long long *scratch, int tid,
+                                                 unsigned long long k0) {
+    const int nt = (int)blockDim.x;
+    unsigned long long *sel_red = scratch;
+    auto tword = [&](int i) { return reinterpret_cast<unsigned *>(&a.sel[(kSelSlots + i) * kSelStride]); };
+    __syncthreads();  // (sel_red[0] may hold k0, read by every thread before this)
+    unsigned long long m = k0;
+    for (int sl = tid; sl < kSelSlots; sl += nt) {
+        unsigned long long *w = &a.sel[sl * kSelStride];
+        const unsigned long long v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        m = v < m ? v : m;
+        __hip_atomic_store(w, kSelNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long t = __shfl_xor(m, o, 64);
+        m = t < m ? t : m;
+    }
+    if ((tid & 63) == 0) sel_red[tid >> 6] = m;
+    __syncthreads();
+    m = sel_red[0];
+    for (int w = 1; w < (nt + 63) / 64; ++w) m = sel_red[w] < m ? sel_red[w] : m;
+    const bool none = m == kSelNone;
+    const long long li = none ? 0 : (long long)(m & 0x7fffffffull) - (a.sel_base & 0x7fffffffll);
+    double *ru = reinterpret_cast<double *>(a.sel_rec + 1);
+    for (int e = tid; e < nV; e += nt) ru[e] = none ? 0.0 : a.U[(size_t)li * nV + e];
+    if (tid <= kSelTickets)
+        __hip_atomic_store(tword(tid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) a.sel_rec[0] = (long long)m;
+}
+
 // Every thread of the workgroup, after its instances' U / cost / status are stored; k (thread
 // 0's) is the workgroup's minimum key; wrote: it stored any instance in this launch.  In the finalizing launch the workgroup that takes the
 // last ticket reduces the slots, copies the winner's U row (written by any workgroup of this or
@@ -114,9 +148,13 @@ constexpr int kSelWords = (kSelSlots + kSelTickets + 1) * kSelStride;
 // call; default the whole grid)
 // tid: the thread index (sel_commit passes threadIdx.x; a one-wave workgroup can pass its lane
 // id, so that threadIdx.x need not live in a register from the kernel's entry)
+// fresh: no workgroup of this launch stored an instance (the overflow list was empty), so every
+// U row the finalizer may copy was stored by an earlier launch on the stream, which the kernel
+// boundary makes visible; with one committing workgroup that finalizer then needs neither the
+// ticket nor the agent-scope fence (~3.5 us of the empty overflow launch's ~8)
 __device__ __forceinline__ void sel_commit_t(const MpcArgs &a, unsigned long long k, int nV,
                                              bool wrote, unsigned long long *scratch, int groups,
-                                             int tid) {
+                                             int tid, bool fresh = false) {
     const int nt = (int)blockDim.x;
     int &sel_last = *reinterpret_cast<int *>(scratch + 16);
     unsigned long long *sel_red = scratch;
@@ -124,6 +162,14 @@ __device__ __forceinline__ void sel_commit_t(const MpcArgs &a, unsigned long lon
     if (!a.sel_final) {  // no-return atomic: the wavefront does not wait for it to complete
         if (tid == 0 && k != kSelNone)
             __hip_atomic_fetch_min(slot, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    if (fresh && groups == 1) {
+        // the one committing workgroup of a launch that stored nothing: its own key (if any)
+        // joins the slots' minimum below directly
+        if (tid == 0) sel_red[0] = k;
+        __syncthreads();
+        sel_final_reduce(a, nV, scratch, tid, sel_red[0]);
         return;
     }
     unsigned long long prev = 0;
@@ -155,33 +201,12 @@ __device__ __forceinline__ void sel_commit_t(const MpcArgs &a, unsigned long lon
     __syncthreads();
     if (!sel_last) return;
     __threadfence();
-    unsigned long long m = kSelNone;
-    for (int sl = tid; sl < kSelSlots; sl += nt) {
-        unsigned long long *w = &a.sel[sl * kSelStride];
-        const unsigned long long v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        m = v < m ? v : m;
-        __hip_atomic_store(w, kSelNone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long t = __shfl_xor(m, o, 64);
-        m = t < m ? t : m;
-    }
-    if ((tid & 63) == 0) sel_red[tid >> 6] = m;
-    __syncthreads();
-    m = sel_red[0];
-    for (int w = 1; w < (nt + 63) / 64; ++w) m = sel_red[w] < m ? sel_red[w] : m;
-    const bool none = m == kSelNone;
-    const long long li = none ? 0 : (long long)(m & 0x7fffffffull) - (a.sel_base & 0x7fffffffll);
-    double *ru = reinterpret_cast<double *>(a.sel_rec + 1);
-    for (int e = tid; e < nV; e += nt) ru[e] = none ? 0.0 : a.U[(size_t)li * nV + e];
-    if (tid <= kSelTickets)
-        __hip_atomic_store(tword(tid), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tid == 0) a.sel_rec[0] = (long long)m;
+    sel_final_reduce(a, nV, scratch, tid, kSelNone);
 }
 __device__ __forceinline__ void sel_commit(const MpcArgs &a, unsigned long long k, int nV,
-                                           bool wrote, unsigned long long *scratch, int groups = -1) {
-    sel_commit_t(a, k, nV, wrote, scratch, groups, (int)threadIdx.x);
+                                           bool wrote, unsigned long long *scratch, int groups = -1,
+                                           bool fresh = false) {
+    sel_commit_t(a, k, nV, wrote, scratch, groups, (int)threadIdx.x, fresh);
 }
 
 // Overflow list (int words).  One counter per 128 B line would still take one device-scope

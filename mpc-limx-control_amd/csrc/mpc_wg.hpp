@@ -183,7 +183,7 @@ __device__ __forceinline__ void wg_mpc_grid(const MpcArgs &a, int *list, int *re
             kmin = k < kmin ? k : kmin;
         }
         sel_commit(a, kmin, NU * N, (int)blockIdx.x < count,
-                   reinterpret_cast<unsigned long long *>(smem), groups);
+                   reinterpret_cast<unsigned long long *>(smem), groups, count <= 0);
     }
 }
 
