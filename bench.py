@@ -83,11 +83,41 @@ def flops_per_qp(p, mean_iters):
     return fl["condense"] + fl["solve_fixed"] + fl["per_iter"] * float(mean_iters)
 
 
-def closed_form_work(p, contact, iters, max_nf):
-    """-> (flops, instances) of the closed-form path's own algorithmic count (mpcqp.flops) over
-    the instances the one-wave kernel solved (nf <= max_nf; the rest are the overflow kernel's)"""
+def algorithmic_work(p, contact, iters, max_nf, solver=None):
+    """-> (algorithmic flops per launch of the fused kernel, instances it solved, basis).
+    Closed-form models (SRBM, literal): the fixed phases (mpcqp/flops.py) over the instances the
+    one-wave kernel solved (nf <= max_nf; the rest are the overflow kernel's), plus the solver's
+    flops -- counted by the paired kernel itself per crash working set and dual pass when
+    `solver` = (flops summed, launches) from mpcqp_solver_flops is given (a working set and a pass
+    cost different amounts, so `iters` alone cannot price them), otherwise priced from `iters` as
+    dual passes (kernels without the crash start).  The dense model (config E) runs the
+    reference's algorithm: SURVEY.md 8d's count."""
     from mpcqp import flops
-    return flops.batch_flops(p, contact, iters, max_nf=max_nf)
+    it = np.asarray(iters)
+    if p["model"] not in (0, 1):
+        return (flops_per_qp(p, float(it.mean())) * len(it), len(it),
+                "SURVEY.md 8d (the dense model runs the reference's Pade expm and condensing)")
+    if solver is not None and solver[1] > 0:
+        fx, n = flops.fixed_flops(p, contact, max_nf)
+        return (fx + solver[0] / solver[1], n,
+                "closed-form fixed phases (mpcqp/flops.py) + the kernel's own count of its crash "
+                "working-set solves and dual passes (mpcqp_count_solver_flops)")
+    fl, n = flops.batch_flops(p, contact, it, max_nf=max_nf)
+    return fl, n, "closed-form fixed phases + dual passes priced from iters (mpcqp/flops.py)"
+
+
+def count_solver_flops(eng, step, sync, launches=3):
+    """(flops, paired-kernel launches) of the kernel's own solver-flops counter over a few more
+    steps after the timed ones (None where the context has no paired kernel)"""
+    if eng.fused_kernel != "k_mpc_pair":
+        return None
+    eng.count_solver_flops(True)
+    for _ in range(launches):
+        step()
+    sync()
+    out = eng.solver_flops()
+    eng.count_solver_flops(False)
+    return out
 
 
 def hbm_fields(traffic, kernel_ms, alg_bytes):
@@ -356,11 +386,18 @@ def time_config(config, B, seed, steps=10, warmup=2, gait=None, device=0):
                max_solver_iters=int(it.max()), solved_frac=float(np.mean(st == 0)))
     if p["model"] in (0, 1):
         # closed-form path: its own algorithmic count over every instance of the call (ms is
-        # the whole solve call, overflow launch included)
-        fl, _ = closed_form_work(p, batch["contact"], it, None)
+        # the whole solve call, overflow launch included); the paired kernel counts its solver
+        # flops itself, in two more launches after the timed ones
+        solver = None
+        if eng.fused_kernel == "k_mpc_pair":
+            eng.count_solver_flops(True)
+            for _ in range(2):
+                eng.solve(d)
+            solver = eng.solver_flops()
+            eng.count_solver_flops(False)
+        fl, _, basis = algorithmic_work(p, batch["contact"], it, None, solver)
         out.update(algorithmic_flops_per_qp=fl / B, achieved_tflops=fl / (ms * 1e-3) / 1e12,
-                   frac=fl / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
-                   flops_basis="closed-form path's algorithmic count (mpcqp/flops.py)",
+                   frac=fl / (ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, flops_basis=basis,
                    work_rate_vs_survey_8d=dict(flops_per_qp=f_qp, tflops=ach8d,
                                                frac=ach8d / FP64_PEAK_TFLOPS))
     else:
@@ -625,6 +662,7 @@ def main():
             mpc_ms = ms / max(1, n)
             sel_ms = 0.0
             eng.enable_timing(False)
+            kern["_solver_flops"] = count_solver_flops(eng, step, sync)
             status = d["status"].cpu().numpy()
             iters = d["iters"].cpu().numpy()
         elif not dry:
@@ -662,6 +700,7 @@ def main():
                     if n:
                         kern[name] = dict(ms=ms / n, launches=n)
                 eng.enable_timing(False)
+                kern["_solver_flops"] = count_solver_flops(eng, step, sync)
             status = d["status"].cpu().numpy()
             iters = d["iters"].cpu().numpy()
         else:
@@ -765,8 +804,11 @@ def main():
         # whole solve in the timed steps (mpc_ms) also hold the overflow launch
         k_ms = kern[eng.fused_kernel]["ms"] if eng.fused_kernel in kern else mpc_ms
         # the work of the instances that kernel solved (an overflow instance is the workgroup
-        # kernel's, timed apart): the closed-form path's own algorithmic count
-        fl, n_solved = closed_form_work(p, local_batch["contact"], iters, eng.pair_nf)
+        # kernel's, timed apart): the closed-form path's own algorithmic count, the solver's
+        # part counted by the kernel (its pass after the timed steps)
+        solver = kern.pop("_solver_flops", None)
+        fl, n_solved, basis = algorithmic_work(p, local_batch.get("contact"), iters, eng.pair_nf,
+                                               solver)
         achieved = fl / (k_ms * 1e-3) / 1e12
         traffic, traffic_tag, traffic_lib = pmc_traffic(args.config, B)
         build = lib_build_id()
@@ -779,15 +821,17 @@ def main():
                    max_solver_iters=int(iters.max()),
                    fast_path=eng.fast_path, select=args.select, kernel_ms=kms,
                    kernel_launches={k: v["launches"] for k, v in kern.items()})
-        alg_bytes = algorithmic_bytes(p["nx"], p["nu"], p["N"]) * B
-        roof = dict(bound="fp64-valu", compute_unit="fp64 VALU (k_mpc_pair issues no MFMA)",
+        alg_bytes = (config_bytes(p) if p["model"] == 2 else
+                     algorithmic_bytes(p["nx"], p["nu"], p["N"])) * B
+        roof = dict(bound="fp64-valu",
+                    compute_unit=("fp64 VALU (k_mpc_pair issues no MFMA)"
+                                  if eng.fused_kernel == "k_mpc_pair" else "fp64 VALU + MFMA"),
                     kernel=eng.fused_kernel, kernel_ms=k_ms, achieved=achieved,
                     peak=FP64_PEAK_TFLOPS, unit="TFLOP/s", frac=achieved / FP64_PEAK_TFLOPS,
                     traffic=traffic,
-                    flops_basis="closed-form path's own algorithmic count (mpcqp/flops.py, "
-                                "DESIGN.md section 4 'Roofline accounting'): model, S blocks, "
-                                "u/v, gradient, H_FF, nf^3/3 Cholesky + nf^3/3 inverse, "
-                                "per-pass dual flops x each instance's passes",
+                    flops_basis=basis + " (DESIGN.md section 4 'Roofline accounting')",
+                    solver_flops_per_launch=(solver[0] / solver[1]) if solver and solver[1]
+                    else None,
                     algorithmic_flops_per_qp=fl / max(1, n_solved), instances=n_solved,
                     work_rate_vs_survey_8d=dict(
                         flops_per_qp=f_qp, tflops=f_qp * B / (k_ms * 1e-3) / 1e12,

@@ -375,6 +375,17 @@ double mpcqp_last_kernel_ms(mpcqp_ctx *ctx, int which);
  * 64; *count receives how many), waiting for them; resets the slot's count.  -1 on error. */
 double mpcqp_kernel_ms_sum(mpcqp_ctx *ctx, int which, int *count);
 
+/* Diagnostic solver-flops counter of the two-QPs-per-wave kernel (k_mpc_pair): with on = 1 every
+ * launch adds the textbook flops of its crash working-set solves and dual passes (mpcqp/flops.py
+ * crash_ws_flops / pass_flops, per instance with its own free count; one atomic per wavefront)
+ * to a context-owned accumulator.  The reported iterations mix working sets and passes, which
+ * cost different amounts, so the headline roofline needs this count (bench.py reads it in a
+ * pass after the timed steps).  mpcqp_solver_flops waits for the stream and returns the sum
+ * since the previous call (-1 if never enabled; *launches: the paired-kernel launches counted),
+ * then resets it.  Other kernels add nothing. */
+int mpcqp_count_solver_flops(mpcqp_ctx *ctx, int on);
+double mpcqp_solver_flops(mpcqp_ctx *ctx, int *launches);
+
 /* Diagnostics: per-phase cycle totals (s_memtime) of the fused kernels since the last call,
  * recorded only by the diagnostic build lib/libmpcqp_stamps.so (first call arms it); the
  * product library returns MPCQP_ERR_BAD_ARG.  Slots: 0 setup, 1 Phi/xf chains, 2 Qe,

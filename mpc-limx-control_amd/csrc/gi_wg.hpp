@@ -183,6 +183,13 @@ __device__ __forceinline__ bool wg_crash(GiCtx &C, const double (&Jr)[NF / 2], d
                                          double &fval, int &iters, double *W) {
     using CL = WgCrashLayout<NF>;
     static_assert(CL::doubles <= WgLayout<NF>::work, "the crash fits the solver's workspace");
+    // after a give-up the dual loop reuses the buffers from oCol on (column broadcast, reflector,
+    // R^-1 slots, multipliers, reductions, active ids) without re-deriving them: the crash's
+    // scratch must stay in the packed L / R region below (NF = 96 fits, the NF = 64
+    // SRBM overflow kernel does not, so MPCQP_WG_SRBM_CRASH=1 builds refuse to compile)
+    static_assert(CL::doubles <= WgLayout<NF>::oCol,
+                  "the crash's scratch overlaps the dual loop's buffers (NF = 64: keep "
+                  "MPCQP_WG_SRBM_CRASH=0)");
     constexpr int KC = CL::KC, NH = NF / 2, RW = WgShape<NF>::RW, NWH = WgShape<NF>::NWH;
     constexpr int NT = 2 * RW, LDW = CL::LDW, LDM = CL::LDM;
     GiLds &L = C.L;

@@ -57,6 +57,9 @@ struct MpcArgs {
     double *U, *cost;
     int *status, *iters;
     unsigned long long *stamps;
+    // diagnostic (mpcqp_count_solver_flops): the paired kernel adds the textbook flops of its
+    // crash working-set solves and dual passes here (one atomic per wavefront); nullptr: off
+    double *flops_acc;
     int cut;  // diagnostic cuts build only
     // device-generated inputs (GEN kernels): instance b = state b / cands,
     // candidate b % cands

@@ -260,6 +260,19 @@ __device__ __forceinline__ void fold_trailing_k(double (&s)[NF], int k, double A
     }
 }
 
+// textbook flops of one crash working-set solve with k bounds and of one dual pass with q
+// constraints active, nf free variables (mpcqp/flops.py, the oracle's t_sflops): the diagnostic
+// solver-flops counter (MpcArgs::flops_acc)
+__device__ __forceinline__ double crash_ws_flops_d(int nf, int k) {
+    const double f = nf, kk = k;
+    return kk * (kk + 1.0) * f + (kk - 1.0) * kk * (kk + 1.0) + 2.0 * kk * f + 2.0 * f * f + f +
+           3.0 * kk;
+}
+__device__ __forceinline__ double pass_flops_d(int nf, int q) {
+    const double f = nf, qq = q, r = nf > q ? (double)(nf - q) : 0.0;
+    return qq * qq + 4.0 * f + 6.0 * f * r + 2.0 * f + 3.0 * qq;
+}
+
 template <int NU, int N, int MODEL, bool GEN>
 __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) {
     static_assert(!GEN || MODEL == 0, "generated inputs are defined for the SRBM model");
@@ -529,6 +542,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     // the batch: B standing's every wavefront) goes straight to the outputs
     double fval = 0.0, x = 0.0;
     int iters = 0;
+    double sfl = 0.0;  // this half's solver flops (diagnostic counter, MpcArgs::flops_acc)
     if (work) {
         // ---- g (lane p: g_p), then H_FF over the dead early view (lane p loads row p)
         const bool ok = valid && status == ST_OK && nf > 0;
@@ -949,6 +963,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 const bool inA = solving && side != 0;
                 if (crashing && k == 0) { xc = x0v; lam = 0.0; fc = f0; }
                 if (solving) ++iters;
+                if (solving) sfl += crash_ws_flops_d(nf, k);
                 const int ks = solving ? k : 0;
                 const int kmax = max(__builtin_amdgcn_readlane(ks, 0), __builtin_amdgcn_readlane(ks, kHalf));
                 if (kmax == 0) continue;  // (wave-uniform)
@@ -1123,6 +1138,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             const bool stepping = go && !done;
             if (stepping) {
                 ++iters;
+                sfl += pass_flops_d(nf, q);
                 // |d(0:q)|^2 and |d(q+1:nf)|^2 in one two-sum pass; zn = |d2|^2 = zq + d_q^2 and
                 // dd = |d|^2 = zn + the first part
                 double sq = hl < q ? dj * dj : 0.0;
@@ -1416,6 +1432,10 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             stream_store(a.status + bo, status);
             stream_store(a.iters + bo, iters);
         }
+    }
+    if (a.flops_acc) {  // (diagnostic) both halves' solver flops, one atomic per wavefront
+        const double t = readlane(sfl, 0) + readlane(sfl, kHalf);
+        if (lno == 0) atomicAdd(a.flops_acc, t);
     }
 #ifndef MPCQP_FUSED_SEL
 #define MPCQP_FUSED_SEL 1

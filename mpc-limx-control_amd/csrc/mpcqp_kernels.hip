@@ -542,6 +542,9 @@ struct mpcqp_ctx {
     double *dAB = nullptr;                  // [B][nx*(nx+nu)] discretised model scratch
     size_t ab_cap = 0;
     unsigned long long *dstamps = nullptr;  // diagnostic phase cycles (stamps build)
+    double *dflops = nullptr;  // diagnostic solver-flops accumulator (mpcqp_count_solver_flops)
+    bool flops_on = false;
+    int flops_launches = 0;
     unsigned long long *dsel = nullptr;     // k_select_min: per-block partial keys + ticket
     int *dlist = nullptr;                   // two overflow lists [count, -, ids...] (mpc_wg.hpp)
     size_t list_cap = 0;                    // instances a list holds
@@ -1000,6 +1003,35 @@ int mpcqp_ctx_crash_params(const mpcqp_ctx *c, int *kmax, int *pmax, int *kmax_w
     return MPCQP_OK;
 }
 
+int mpcqp_count_solver_flops(mpcqp_ctx *c, int on) {
+    if (!c) return MPCQP_ERR_BAD_ARG;
+    if (on && !c->dflops) {
+        hipSetDevice(c->device);
+        if (hipMalloc(&c->dflops, sizeof(double)) != hipSuccess ||
+            hipMemset(c->dflops, 0, sizeof(double)) != hipSuccess) {
+            hipFree(c->dflops);
+            c->dflops = nullptr;
+            return MPCQP_ERR_DEVICE;
+        }
+    }
+    c->flops_on = on != 0;
+    return MPCQP_OK;
+}
+
+double mpcqp_solver_flops(mpcqp_ctx *c, int *launches) {
+    if (launches) *launches = 0;
+    if (!c || !c->dflops) return -1.0;
+    double v = 0.0;
+    hipSetDevice(c->device);
+    if (hipStreamSynchronize(c->stream) != hipSuccess ||
+        hipMemcpy(&v, c->dflops, sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemset(c->dflops, 0, sizeof(double)) != hipSuccess)
+        return -1.0;
+    if (launches) *launches = c->flops_launches;
+    c->flops_launches = 0;
+    return v;
+}
+
 int mpcqp_debug_phase_cycles(mpcqp_ctx *c, uint64_t *out, int n) {
 #ifdef MPCQP_STAMPS
     if (!c || !out || n <= 0) return MPCQP_ERR_BAD_ARG;
@@ -1037,6 +1069,7 @@ int mpcqp_ctx_destroy(mpcqp_ctx *c) {
     hipFree(c->dFP);
     hipFree(c->dAB);
     hipFree(c->dstamps);
+    hipFree(c->dflops);
     hipFree(c->dsel);
     hipFree(c->dlist);
     hipFree(c->hbuf);
@@ -1207,6 +1240,7 @@ static MpcArgs mpc_args(mpcqp_ctx *c, int B) {
         a.thi_t = -kFeasTol * (1.0 + fabs(a.bhi_t));
     }
     a.stamps = c->dstamps;
+    a.flops_acc = c->flops_on ? c->dflops : nullptr;
     a.cut = 0;
 #ifdef MPCQP_CUTS
     if (const char *e = getenv("MPCQP_CUT")) a.cut = atoi(e);
@@ -1301,6 +1335,7 @@ static int launch_mpc(mpcqp_ctx *c, bool gen, int B, MpcArgs *a, bool may_overfl
     }
     const void *pk = gen ? c->fk.pair_gen : c->fk.pair;
     a->sel_final = a->ovf ? 0 : 1;  // fused selection: the batch's last launch finalizes
+    if (a->flops_acc && pk) ++c->flops_launches;
     tbegin(c, 2);
     int rc = pk ? launch(pk, (B + 1) / 2, c->fk.pair_lds, c->stream, a)
                 : launch(gen ? c->fk.mpc_gen : c->fk.mpc, B, c->fk.mpc_lds, c->stream, a);

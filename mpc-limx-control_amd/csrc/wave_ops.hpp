@@ -214,8 +214,13 @@ __device__ __forceinline__ void step_fence() {
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// 1/sqrt(a) for a > 0: v_rsq_f64 plus two Newton steps (~1 ulp; a short dependency chain
-// compared with the correctly rounded sqrt and divide sequences)
+// 1/sqrt(a) for a > 0: v_rsq_f64 plus MPCQP_RSQ_NR Newton steps -- a short dependency chain
+// compared with the correctly rounded sqrt and divide sequences.  v_rsq_f64 is good to about
+// 2^-23 relative; each step squares the error: one step (the default) gives about 2^-46 (tens of
+// ulp, ~1e-14 relative) in every Cholesky pivot scale, two steps ~1 ulp.  The factor is then
+// L (1 + e) column-wise with |e| ~ 1e-14 and J its exact inverse, so H^-1 = J J' carries ~1e-14
+// relative error: four orders below the parity tolerance (1e-8 max(1, |U|)); the ill-conditioned
+// parity case tests/test_gpu_parity.py::test_pair_kernel_ill_conditioned_vs_oracle guards it.
 #ifndef MPCQP_RSQ_NR
 // Newton steps after v_rsq_f64 (its estimate is good to about half the mantissa; one step squares
 // the error): 1 since r04 -- parity suite unchanged, B 315 -> 311 us, L 2.38 -> 2.34 ms,

@@ -26,6 +26,7 @@ EXPORTS = [
     "mpcqp_batch_condense", "mpcqp_batch_solve_qp", "mpcqp_batch_solve",
     "mpcqp_ctx_fast_path", "mpcqp_ctx_one_wave_nf", "mpcqp_ctx_crash_params", "mpcqp_batch_discretize", "mpcqp_batch_condense_solve",
     "mpcqp_debug_phase_cycles", "mpcqp_batch_solve_host",
+    "mpcqp_count_solver_flops", "mpcqp_solver_flops",
     "mpcqp_batch_select_min", "mpcqp_batch_select_record", "mpcqp_reduce_records",
     "mpcqp_batch_solve_select",
     "mpcqp_enable_timing", "mpcqp_last_kernel_ms", "mpcqp_kernel_ms_sum",
@@ -86,6 +87,10 @@ def lib():
         if hasattr(L, name):  # absent from A/B builds of older sources
             getattr(L, name).argtypes = at
     L.mpcqp_debug_phase_cycles.argtypes = [vp, vp, i]
+    if hasattr(L, "mpcqp_count_solver_flops"):  # absent from A/B builds of older sources
+        L.mpcqp_count_solver_flops.argtypes = [vp, i]
+        L.mpcqp_solver_flops.argtypes = [vp, C.POINTER(C.c_int)]
+        L.mpcqp_solver_flops.restype = C.c_double
     L.mpcqp_batch_solve_host.argtypes = [vp, i] + [vp] * 8
     L.mpcqp_batch_discretize.argtypes = [vp, i, vp, vp]
     L.mpcqp_batch_condense_solve.argtypes = [vp, i] + [vp] * 8

@@ -240,6 +240,16 @@ class BatchEngine:
     def enable_timing(self, on=True):
         check("mpcqp_enable_timing", lib().mpcqp_enable_timing(self.ctx, 1 if on else 0))
 
+    def count_solver_flops(self, on=True):
+        """(diagnostic) k_mpc_pair adds its crash working-set and dual-pass flops to a counter"""
+        check("mpcqp_count_solver_flops", lib().mpcqp_count_solver_flops(self.ctx, 1 if on else 0))
+
+    def solver_flops(self):
+        """(flops summed since the previous call, paired-kernel launches counted); waits"""
+        n = C.c_int(0)
+        v = float(lib().mpcqp_solver_flops(self.ctx, C.byref(n)))
+        return v, n.value
+
     def last_kernel_ms(self, which: int) -> float:
         """which: 0 stage 1, 1 the whole solve, 2 the one-wave fused kernel, 3 the overflow
         workgroup kernel (mpcqp.h)"""

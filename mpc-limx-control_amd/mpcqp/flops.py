@@ -25,6 +25,19 @@ literal 13x3 model: 3), N steps, NU inputs per step:
               updates (2 nf + 3 q), the Householder add J2 <- J2 (I - beta v v')
               (4 nf (nf - q)); a friction row's normal has two nonzeros (+2 nf)
 
+  crash set   (k_mpc_pair's crash start, one working set of k bounds solved): the Gram
+              M = J_A J_A' (k(k+1)/2 entries of nf-long dots), Gauss-Jordan with one right-hand
+              side ((k-1) k (k+1)), w (k), y = J_A' w (2 k nf), x = x0 - J y (2 nf^2), the
+              x / f updates (nf + 2k)
+
+A pass and a working-set solve cost different amounts, and an instance's `iters` counts both,
+so the headline kernel's solver flops are not a function of `iters`: k_mpc_pair counts them
+itself, per working set and pass, when its context asks for it (mpcqp_count_solver_flops, a
+diagnostic pointer; bench.py's pass after the timed steps), with exactly these formulas; the
+oracle applies the same formulas to its own decisions (oracle.srbm_batch(want_flops=True)).
+Kernels without the crash start (configs C, L: k_mpc) report dual passes only, which
+`batch_flops` prices from `iters`.
+
 The SIMD kernel executes more FP64 instructions than this (lane l owns row l, so every
 triangular sweep runs its square; pad lanes; EXEC-masked halves): `roofline.pipe_frac`
 (rocprofv3 SQ_INSTS_VALU_FLOPS_FP64 x 64 lanes) is that executed rate, and
@@ -69,6 +82,21 @@ def pass_flops(nf: int, q: int, friction: bool = False) -> float:
     """one dual add pass with q constraints already active"""
     r = max(0, nf - q)
     return q * q + 4 * nf + 2 * nf * r + 2 * nf + 3 * q + 4 * nf * r + (2 * nf if friction else 0)
+
+
+def crash_ws_flops(nf: int, k: int) -> float:
+    """one crash working-set solve with k bounds (the kernel's and the oracle's formula)"""
+    return k * (k + 1) * nf + (k - 1) * k * (k + 1) + 2 * k * nf + 2 * nf * nf + nf + 3 * k
+
+
+def fixed_flops(p: dict, contact, max_nf: int | None = None):
+    """-> (flops of the phases before the solver over the instances the one-wave kernel solved,
+    their count): add the kernel-counted solver flops for the headline kernel's total"""
+    nf = free_counts(p, contact)
+    keep = nf > 0 if max_nf is None else (nf > 0) & (nf <= max_nf)
+    vals, counts = np.unique(nf[keep], return_counts=True)
+    return float(sum(c * sum(fixed_phases(p, int(f)).values()) for f, c in zip(vals, counts))), \
+        int(keep.sum())
 
 
 def instance_flops(p: dict, nf: int, iters: int) -> float:

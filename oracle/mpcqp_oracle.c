@@ -421,6 +421,22 @@ typedef struct {
  * same point the dual active-set loop reaches.  Gives up (returns 0, x / fval untouched) after
  * pmax working sets or a non-positive pivot: the caller then runs Goldfarb-Idnani from x0.
  * *solves counts the working sets that needed a solve (the reported iterations). */
+/* Solver flops of the instance being solved on this thread (orc_srbm_batch's sflops output),
+ * counted the textbook way per working-set solve and per dual pass -- the same formulas the
+ * paired kernel's diagnostic counter applies (mpcqp/flops.py crash_ws_flops / pass_flops). */
+static _Thread_local double t_sflops;
+static double crash_ws_flops(int nf, int k) {
+    /* Gram M = J_A J_A' (k(k+1)/2 entries, nf-long dots), Gauss-Jordan with one right-hand side,
+     * w, y = J_A' w, x = x0 - J y, f */
+    return (double)k * (k + 1) * nf + (double)(k - 1) * k * (k + 1) + 2.0 * k * nf +
+           2.0 * nf * nf + nf + 3.0 * k;
+}
+static double pass_flops(int nf, int q, int friction_row) {
+    const double r = (double)(nf - q > 0 ? nf - q : 0);
+    return (double)q * q + 4.0 * nf + 2.0 * nf * r + 2.0 * nf + 3.0 * q + 4.0 * nf * r +
+           (friction_row ? 2.0 * nf : 0.0);
+}
+
 static int box_crash(int n, const double *J, const double *x0, double fval0, const gi_cons *C,
                      int kmax, int pmax, double *x, double *fval, double *u_cons, int *solves) {
     int *lo_c = malloc(sizeof(int) * 2 * n), *up_c = lo_c + n;
@@ -480,6 +496,7 @@ static int box_crash(int n, const double *J, const double *x0, double fval0, con
             continue;
         }
         ++ns;
+        t_sflops += crash_ws_flops(n, k);
         for (int i = 0; i < k; ++i) {
             for (int m = 0; m < k; ++m) {
                 double s = 0.0;
@@ -640,6 +657,7 @@ static int gi_solve(int n, double *Hf /* n x n, destroyed */, const double *g, g
         for (;;) {
             if (iters >= max_iter) { status = ORC_ITER_LIMIT; goto done; }
             ++iters;
+            t_sflops += pass_flops(n, q, C->src[p] >= 2 * n);
             double dd = 0.0, zn = 0.0;
             for (int j = 0; j < n; ++j) {
                 double s = 0.0;
@@ -1056,7 +1074,8 @@ static int srbm_one(const orc_srbm_cfg *cfg, const double *x0, const double *xre
 
 int orc_srbm_batch(const orc_srbm_cfg *cfg, int B, const double *x0, const double *xref,
                    const double *lin, const uint64_t *contact, double *U, double *cost,
-                   int *status, int *iters, double *H_out, double *f_out, int nthreads) {
+                   int *status, int *iters, double *H_out, double *f_out, int nthreads,
+                   double *sflops) {
     const int nx = cfg->nx, nV = cfg->nu * cfg->N;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -1065,6 +1084,7 @@ int orc_srbm_batch(const orc_srbm_cfg *cfg, int B, const double *x0, const doubl
     for (int b = 0; b < B; ++b) {
         int it = 0;
         double c = 0.0;
+        t_sflops = 0.0;
         const int st = srbm_one(cfg, x0 + (size_t)b * nx, xref + (size_t)b * nx * (cfg->N + 1),
                                 lin + (size_t)b * 8, contact[b], U + (size_t)b * nV, &c, &it,
                                 H_out ? H_out + (size_t)b * nV * nV : NULL,
@@ -1072,6 +1092,7 @@ int orc_srbm_batch(const orc_srbm_cfg *cfg, int B, const double *x0, const doubl
         if (cost) cost[b] = c;
         if (status) status[b] = st;
         if (iters) iters[b] = it;
+        if (sflops) sflops[b] = t_sflops;
     }
     (void)nthreads;
     return ORC_OK;

@@ -120,7 +120,9 @@ typedef struct {
 int orc_srbm_batch(const orc_srbm_cfg *cfg, int B, const double *x0, const double *xref,
                    const double *lin, const uint64_t *contact, double *U, double *cost,
                    int *status, int *iters, double *H_out /* nullable [B][nV][nV] */,
-                   double *f_out /* nullable [B][nV] */, int nthreads);
+                   double *f_out /* nullable [B][nV] */, int nthreads,
+                   double *sflops /* nullable [B]: solver flops per instance (crash working-set
+                                     solves + dual passes, mpcqp/flops.py formulas) */);
 
 /* per-instance bounds of the SRBM model (contact schedule -> lb/ub) */
 void orc_srbm_bounds(const orc_srbm_cfg *cfg, uint64_t contact, double *lb, double *ub);

@@ -81,7 +81,7 @@ def lib():
         L.orc_gait_contact_mask.argtypes = [C.c_int, C.c_double, C.c_double, C.c_float, C.c_float]
         L.orc_gait_contact_mask.restype = C.c_uint64
         L.orc_srbm_batch.argtypes = [C.POINTER(SrbmCfg), C.c_int, _dp, _dp, _dp, _up, _dp, _dp,
-                                     _ip, _ip, C.c_void_p, C.c_void_p, C.c_int]
+                                     _ip, _ip, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
         L.orc_dense_batch.argtypes = [C.POINTER(DenseCfg), C.c_int, _dp, _dp, _dp, _dp, _dp, _ip,
                                       _ip, C.c_void_p, C.c_void_p, C.c_int]
         L.orc_srbm_bounds.argtypes = [C.POINTER(SrbmCfg), C.c_uint64, _dp, _dp]
@@ -215,7 +215,7 @@ def make_cfg(p):
     return cfg, keep
 
 
-def srbm_batch(p, x0, xref, lin, contact, nthreads=0, want_hf=False):
+def srbm_batch(p, x0, xref, lin, contact, nthreads=0, want_hf=False, want_flops=False):
     cfg, keep = make_cfg(p)
     B = int(x0.shape[0])
     nV = p["nu"] * p["N"]
@@ -225,16 +225,19 @@ def srbm_batch(p, x0, xref, lin, contact, nthreads=0, want_hf=False):
     iters = np.zeros(B, np.int32)
     H = np.zeros(B * nV * nV) if want_hf else None
     f = np.zeros(B * nV) if want_hf else None
+    sfl = np.zeros(B) if want_flops else None
     lib().orc_srbm_batch(C.byref(cfg), B, np.ascontiguousarray(x0, dtype=np.float64).reshape(-1),
                          np.ascontiguousarray(xref, dtype=np.float64).reshape(-1),
                          np.ascontiguousarray(lin, dtype=np.float64).reshape(-1),
                          np.ascontiguousarray(contact, dtype=np.uint64), U, cost, status, iters,
-                         _ptr(H), _ptr(f), int(nthreads))
+                         _ptr(H), _ptr(f), int(nthreads), _ptr(sfl))
     del keep
     out = dict(U=U.reshape(B, nV), cost=cost, status=status, iters=iters)
     if want_hf:
         out["H"] = H.reshape(B, nV, nV).transpose(0, 2, 1)  # column-major per instance
         out["f"] = f.reshape(B, nV)
+    if want_flops:
+        out["solver_flops"] = sfl
     return out
 
 

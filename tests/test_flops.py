@@ -53,3 +53,42 @@ def test_batch_accounting():
     assert flops.instance_flops(p, 30, 2) > flops.instance_flops(p, 30, 1)
     t = flops.phase_table(p, 30, 2.0)
     assert t["total"] == pytest.approx(flops.instance_flops(p, 30, 2))
+
+
+def test_crash_working_set_formula_and_fixed_flops():
+    # Gram k(k+1) nf, Gauss-Jordan (k-1) k (k+1), w k, y 2 k nf, x 2 nf^2, x / f nf + 2k
+    assert flops.crash_ws_flops(30, 1) == 2 * 30 + 0 + 2 * 30 + 2 * 900 + 30 + 3
+    assert flops.crash_ws_flops(30, 10) == 110 * 30 + 9 * 10 * 11 + 600 + 1800 + 30 + 30
+    # a working set is cheaper than the dual passes it replaces (k adds from q = 0)
+    assert flops.crash_ws_flops(30, 4) < sum(flops.pass_flops(30, q) for q in range(4))
+    p = mpcqp.model_params("B")
+    N = p["N"]
+    one_foot = sum(1 << (2 * k) for k in range(N))
+    contact = np.array([one_foot, one_foot, (1 << (2 * N)) - 1, 0], dtype=np.uint64)
+    fx, n = flops.fixed_flops(p, contact, 30)
+    assert n == 2 and fx == pytest.approx(2 * sum(flops.fixed_phases(p, 30).values()))
+
+
+def test_bench_algorithmic_work_every_model():
+    """bench.py's roofline count for each headline model: closed form + the kernel's solver
+    count (B), closed form + passes from iters (no count), SURVEY 8d for the dense model (E:
+    ADVICE r04 -- the closed form has no support rows for it)"""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "bench", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    p = mpcqp.model_params("B")
+    b = mpcqp.make_batch(p, 64, seed=3)
+    it = np.zeros(64, np.int32)
+    fx, n = flops.fixed_flops(p, b["contact"], 30)
+    fl, n2, basis = bench.algorithmic_work(p, b["contact"], it, 30, solver=(6.4e5, 2))
+    assert n2 == n and fl == pytest.approx(fx + 3.2e5) and "count" in basis
+    fl0, _, basis0 = bench.algorithmic_work(p, b["contact"], it, 30)
+    assert fl0 == pytest.approx(fx) and "iters" in basis0
+    e = mpcqp.model_params("E")
+    be = mpcqp.make_batch(e, 32, seed=3)
+    it_e = np.full(32, 3, np.int32)
+    fl_e, n_e, basis_e = bench.algorithmic_work(e, be["contact"], it_e, 0)
+    assert n_e == 32 and "8d" in basis_e
+    assert fl_e == pytest.approx(bench.flops_per_qp(e, 3.0) * 32)

@@ -202,3 +202,30 @@ def test_rollout_warm_start_matches_oracle_and_saves_passes(gpu, orc):
     cold = _closed_loop_iters(p, g, K, False)
     assert warm[0] == cold[0]
     assert warm[1:].sum() < 0.9 * cold[1:].sum(), (warm, cold)
+
+
+@pytest.mark.gpu
+def test_pair_kernel_solver_flops_count_matches_oracle(gpu, orc):
+    """k_mpc_pair's diagnostic solver-flops counter (mpcqp_count_solver_flops: crash working-set
+    solves and dual passes, per instance with its own free count) against the oracle's count of
+    the same formulas over its own decisions with the kernel's crash caps (iteration counts
+    agree on >= 99 % of instances, so the totals agree closely)"""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("B")
+    b = mpcqp.make_batch(p, 4096, seed=91)
+    eng = BatchEngine(p)
+    d = eng.upload(b)
+    eng.count_solver_flops(True)
+    eng.solve(d)
+    got, launches = eng.solver_flops()
+    eng.count_solver_flops(False)
+    assert launches == 1
+    eng.solve(d)  # counting off: nothing added
+    assert eng.solver_flops() == (0.0, 0)
+    pc = dict(p)
+    pc["crash"] = eng.crash
+    ref = orc.srbm_batch(pc, b["x0"], b["xref"], b["lin"], b["contact"], want_flops=True)
+    eng.close()
+    want = float(ref["solver_flops"].sum())
+    assert want > 0 and abs(got - want) <= 0.01 * want, (got, want)
