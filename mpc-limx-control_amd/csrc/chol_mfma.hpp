@@ -57,7 +57,75 @@ __device__ __forceinline__ int tix(int i, int j) { return i * (i + 1) / 2 + j; }
 #ifndef MPCQP_DIAG_NOSEL
 #define MPCQP_DIAG_NOSEL 1
 #endif
+// MPCQP_DIAG_DPP: every 16-lane row of the wave factors the same block (lane i of each row owns
+// row i), and step k's broadcast L(j, k) comes from lane j of the lane's own row inside the FMA
+// (v_fmac_f64_dpp row_newbcast), instead of 120 v_readlane pairs per block whose SGPR results
+// spilled to VGPR lanes.  Same operations in the same order per element (bit-identical).
+// 0: the v_readlane form (A/B builds).
+#ifndef MPCQP_DIAG_DPP
+#define MPCQP_DIAG_DPP 1
+#endif
+// acc -= (lane J of this lane's 16-lane row of b) * m; NOP: give b its two wait states after the
+// VALU that wrote it
+template <int J, bool NOP>
+__device__ __forceinline__ void fmac_rowbcast_neg(double &acc, double b, double m) {
+    if constexpr (NOP)
+        asm("s_nop 1\n\tv_fmac_f64_dpp %0, -%1, %2 row_newbcast:%c3 row_mask:0xf bank_mask:0xf"
+            : "+v"(acc) : "v"(b), "v"(m), "i"(J));
+    else
+        asm("v_fmac_f64_dpp %0, -%1, %2 row_newbcast:%c3 row_mask:0xf bank_mask:0xf"
+            : "+v"(acc) : "v"(b), "v"(m), "i"(J));
+}
+// step K's updates of row entries and W columns j = J .. 15 (J = K + 1 first)
+template <int K, int J = K + 1>
+__device__ __forceinline__ void diag_step_dpp(double (&a)[16], double (&w)[16], double lk) {
+    if constexpr (J < 16) {
+        fmac_rowbcast_neg<J, J == K + 1>(a[J], lk, lk);     // a[j] -= L(j, k) L(ln, k)
+        fmac_rowbcast_neg<J, false>(w[J], lk, w[K]);         // w[j] -= L(j, k) w[k]
+        diag_step_dpp<K, J + 1>(a, w, lk);
+    }
+}
+template <int K = 0>
+__device__ __forceinline__ void diag_factor_dpp(double (&a)[16], double (&w)[16], bool &bad) {
+    if constexpr (K < 16) {
+        const double piv = dpp<0x150 + K>(a[K]);  // lane K of the row (row_newbcast)
+        bad |= !(piv > 0.0);
+        const double isq = rsqrt_nr(piv);
+        const double lk = a[K] * isq;
+        a[K] = lk;
+        w[K] *= isq;
+        diag_step_dpp<K>(a, w, lk);
+        diag_factor_dpp<K + 1>(a, w, bad);
+    }
+}
+__device__ __forceinline__ void diag_block_inverse_rl(double *tile, double *wt, bool &bad);
 __device__ __forceinline__ void diag_block_inverse(double *tile, double *wt, bool &bad) {
+#if MPCQP_DIAG_DPP
+    const int ln = lane();
+    const int li = ln & 15;
+    double a[16], w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        a[j] = (j <= li) ? tile[64 * (li >> 2) + 16 * (li & 3) + j] : 0.0;
+        w[j] = (li == j) ? 1.0 : 0.0;
+    }
+    // (every row computes the same pivots; the ballot keeps the flag wave-uniform for the
+    //  compiler, which otherwise treats the solver's status as divergent from here on)
+    bool nb = false;
+    diag_factor_dpp(a, w, nb);
+    bad |= __ballot(nb) != 0ull;
+    if (ln < 16) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            tile[64 * (i >> 2) + 16 * (i & 3) + li] = w[i];   // W(i, c), c = li
+            wt[64 * (li >> 2) + 16 * (li & 3) + i] = w[i];    // W'(c, i)
+        }
+    }
+    return;
+#endif
+    diag_block_inverse_rl(tile, wt, bad);
+}
+__device__ __forceinline__ void diag_block_inverse_rl(double *tile, double *wt, bool &bad) {
     const int ln = lane();
     const bool on = ln < 16;
     const int li = ln & 15;
