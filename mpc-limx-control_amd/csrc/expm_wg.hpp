@@ -436,8 +436,14 @@ __device__ __forceinline__ void wg_expm(int nx, int ns, double *T, double *ws, d
     }
     MPCQP_STAMP(stamps, 12, tx);
     if (MPCQP_PADE_WAVE && nx == 24 && nx + ns <= kWave) {  // config E
+#ifdef MPCQP_PADE_PROBE  // (stamps build only) wave 0's solve in slot 15, the side work in slot 0
+        MPCQP_STAMP_INIT(tp);
+        if (wv == 0) { wave_pade_gj<24>(ns, U, V, E, A2); MPCQP_STAMP(stamps, 15, tp); }
+        else if (wv == nw - 1) { side(); MPCQP_STAMP(stamps, 0, tp); }
+#else
         if (wv == 0) wave_pade_gj<24>(ns, U, V, E, A2);  // A2 .. W are dead here
         else if (wv == nw - 1) side();
+#endif
     } else if (nx <= 6 * nw && nx + ns <= kWave && 4 * sz >= 352) {  // A2 .. W are dead here
         wg_pade_solve<6>(nx, ns, U, V, E, A2, wv, nw);         // config E: 24 rows, 4 waves
     } else if (nx <= 8 * nw && nx + ns <= kWave && 4 * sz >= 352) {

@@ -324,19 +324,20 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
             // ---- step 1: most violated inactive constraint (lowest id on ties)
             double best = INFINITY;
             int bid = 0x7fffffff;
+            const bool qsel = C.nfric > 0 && P.contact != 0ull;  // (gi_sel_key)
             if (ln < nf) {
                 const unsigned char s0 = L.st[ln], s1 = L.st[ln + nf];
                 const double b0 = L.cb[ln], b1 = L.cb[ln + nf];
                 if (s0 == 1) {
                     const double sl_ = x - b0;
                     if (sl_ < -kFeasTol * (1.0 + fabs(b0))) {
-                        best = (gmask & 1) ? -INFINITY : sl_;
+                        best = (gmask & 1) ? -INFINITY : gi_sel_key(sl_, qsel);
                         bid = ln;
                     }
                 }
                 if (s1 == 1) {
                     const double sl_ = -x - b1;
-                    const double kv = (gmask & 2) ? -INFINITY : sl_;
+                    const double kv = (gmask & 2) ? -INFINITY : gi_sel_key(sl_, qsel);
                     if (sl_ < -kFeasTol * (1.0 + fabs(b1)) && kv < best) { best = kv; bid = ln + nf; }
                 }
             }
@@ -351,7 +352,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
                         s += P.mu * x;
                         s += sg * ((t >> 1) ? xm1 : xm2);
                         const double sl_ = s - 0.0;
-                        const double kv = (gmask & (4 << t)) ? -INFINITY : sl_;
+                        const double kv = (gmask & (4 << t)) ? -INFINITY : gi_sel_key(sl_, qsel);
                         if (sl_ < -kFeasTol * (1.0 + fabs(0.0)) && kv < best) { best = kv; bid = fbase + t; }
                     }
                 }

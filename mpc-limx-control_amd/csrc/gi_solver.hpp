@@ -144,6 +144,17 @@ __device__ __forceinline__ void var_bounds(const SolveProblem &P, int v, double 
     hi = P.ub ? P.ub[v] : kInfty;
 }
 
+// The most-violated selection's key when the QP has friction rows (qsel = nfric > 0 and a foot
+// in contact): the violation with its low 20 mantissa bits cleared, so violations within ~2^-32
+// relative tie and the lowest id wins, as for exact ties.  A pyramid's +- rows are exactly tied
+// whenever the tangential force is zero, and rounding alone would otherwise pick one of them,
+// differently here and in the oracle (gi_sel_key, oracle/mpcqp_oracle.c): same minimiser,
+// different pass counts.  Box-only problems compare the violations themselves.
+__device__ __forceinline__ double gi_sel_key(double s, bool qsel) {
+    const long long b = __double_as_longlong(s) & ~0xFFFFFll;
+    return qsel ? __longlong_as_double(b) : s;
+}
+
 // ---------------------------------------------------------------- constraint accessors
 // b of the one-sided constraint id (normal' x_F >= b, fixed parts folded into b)
 __device__ __forceinline__ double gi_cons_b(const GiCtx &C, int id) {
@@ -243,6 +254,11 @@ __device__ __forceinline__ void gi_cons_project(const GiCtx &C, int id, double x
 }
 
 // ---------------------------------------------------------------- stage 1: setup
+// MPCQP_ELIDE_FZ: leave out a contact foot's fz lower bound that its friction pyramid implies
+// (see gi_setup); 0 keeps it (A/B builds -- the oracle then needs p["elide_fz"] = 0)
+#ifndef MPCQP_ELIDE_FZ
+#define MPCQP_ELIDE_FZ 1
+#endif
 // Fixed variables, free index map, constraint states.  Leaves C.nf, C.mt, C.status.
 __device__ __forceinline__ void gi_setup(GiCtx &C) {
     const SolveProblem &P = *C.P;
@@ -280,8 +296,18 @@ __device__ __forceinline__ void gi_setup(GiCtx &C) {
         unsigned char s = 0;
         if (id < 2 * nf) {
             double lo, hi;
-            var_bounds(P, L.fid[id < nf ? id : id - nf], lo, hi);
+            const int v = L.fid[id < nf ? id : id - nf];
+            var_bounds(P, v, lo, hi);
             s = (id < nf) ? (lo > -kInfty ? 1 : 0) : (hi < kInfty ? 1 : 0);
+            // the lower bound fz >= lo <= 0 of a foot in contact is implied by its friction
+            // pyramid (mu fz -+ fx >= 0 sum to fz >= 0): left out, the same feasible set and
+            // minimiser without the degenerate apex where five constraints meet in 3-D (the
+            // dual loop's add / drop cycles there: config C's mean passes 5.9 -> 2.8 in the
+            // oracle); the oracle does the same (orc_friction::elide_fz)
+            if (MPCQP_ELIDE_FZ && id < nf && nfric > 0 && s == 1 && lo <= 0.0) {
+                const int k = v / P.nu, c = v % P.nu;
+                if (c % 3 == 2 && c / 3 < P.nfeet && ((P.contact >> (2 * k + c / 3)) & 1ull)) s = 0;
+            }
         } else if (id < 2 * nf + nfric) {
             const int r = id - 2 * nf, ks = r >> 2, t = r & 3;
             const int k = ks / P.nfeet, sft = ks % P.nfeet;
@@ -446,7 +472,8 @@ __device__ __forceinline__ void gi_run(GiCtx &C) {
             for (int id = ln; id < mt; id += kWave) {
                 if (L.st[id] != 1) continue;
                 const double s = gi_cons_slack_lane(C, id);
-                if (s < -kFeasTol * (1.0 + fabs(gi_cons_b(C, id))) && s < best) { best = s; bid = id; }
+                const double key = gi_sel_key(s, C.nfric > 0 && P.contact != 0ull);
+                if (s < -kFeasTol * (1.0 + fabs(gi_cons_b(C, id))) && key < best) { best = key; bid = id; }
             }
             wave_argmin(best, bid);
             if (bid == 0x7fffffff) break;  // optimal

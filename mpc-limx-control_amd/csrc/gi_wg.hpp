@@ -463,16 +463,18 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
             // ---- step 1: most violated inactive constraint (lowest id on ties)
             double best = INFINITY;
             int bid = 0x7fffffff;
+            const bool qsel = C.nfric > 0 && P.contact != 0ull;  // (gi_sel_key)
             if (h == 0 && r < nf) {
                 const int s0 = kStReg ? s0r : L.st[r], s1 = kStReg ? s1r : L.st[r + nf];
                 const double b0 = kStReg ? b0r : L.cb[r], b1 = kStReg ? b1r : L.cb[r + nf];
                 if (s0 == 1) {
                     const double sl_ = x - b0;
-                    if (sl_ < -kFeasTol * (1.0 + fabs(b0))) { best = sl_; bid = r; }
+                    if (sl_ < -kFeasTol * (1.0 + fabs(b0))) { best = gi_sel_key(sl_, qsel); bid = r; }
                 }
                 if (s1 == 1) {
                     const double sl_ = -x - b1;
-                    if (sl_ < -kFeasTol * (1.0 + fabs(b1)) && sl_ < best) { best = sl_; bid = r + nf; }
+                    const double kv = gi_sel_key(sl_, qsel);
+                    if (sl_ < -kFeasTol * (1.0 + fabs(b1)) && kv < best) { best = kv; bid = r + nf; }
                 }
                 if (fbase >= 0) {
                     const double xm1 = L.xs[r - 1], xm2 = L.xs[r - 2];  // fy, fx of the foot
@@ -483,7 +485,8 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
                         double s = 0.0;
                         s += P.mu * x;
                         s += sg * ((t >> 1) ? xm1 : xm2);
-                        if (s < -kFeasTol && s < best) { best = s; bid = fbase + t; }
+                        const double kv = gi_sel_key(s, qsel);
+                        if (s < -kFeasTol && kv < best) { best = kv; bid = fbase + t; }
                     }
                 }
             }

@@ -407,7 +407,22 @@ typedef struct {
     double *b;    /* m */
     int *is_eq;   /* m */
     int *src;     /* m: original constraint id (see ordering above) */
+    int qsel;     /* friction rows present: selection keys quantized (gi_sel_key) */
 } gi_cons;
+
+/* The most-violated selection's key when the QP has friction rows: the violation with its low
+ * 20 mantissa bits cleared, so violations within ~2^-32 relative tie and the lowest id wins, as
+ * for exact ties.  A pyramid's +- rows are exactly tied whenever the tangential force is zero
+ * (symmetric commands), and rounding alone would otherwise pick one of them -- differently in
+ * the library's solvers and here (same minimiser, different pass counts).  The library's
+ * one-wave and workgroup solvers use the same key (gi_sel_key, gi_solver.hpp). */
+static double gi_sel_key(double s) {
+    uint64_t u;
+    memcpy(&u, &s, sizeof u);
+    u &= ~(uint64_t)0xFFFFF;
+    memcpy(&s, &u, sizeof u);
+    return s;
+}
 
 /* Speculative primal-dual active-set start for problems whose constraints are all bounds (the
  * GPU kernels' "crash").  From the unconstrained minimum x0 (H^-1 = J J'):
@@ -643,13 +658,14 @@ static int gi_solve(int n, double *Hf /* n x n, destroyed */, const double *g, g
                 const double *nc = C->N + (size_t)c * n;
                 double s = -C->b[c];
                 for (int i = 0; i < n; ++i) s += nc[i] * x[i];
-                if (s < -GI_FEAS_TOL * (1.0 + fabs(C->b[c])) && (p < 0 || s < best)) {
-                    best = s;
+                const double key = C->qsel ? gi_sel_key(s) : s;
+                if (s < -GI_FEAS_TOL * (1.0 + fabs(C->b[c])) && (p < 0 || key < best)) {
+                    best = key;
+                    sp = s;
                     p = c;
                 }
             }
             if (p < 0) break; /* optimal */
-            sp = best;
         }
         const double *np = C->N + (size_t)p * n;
         u[q] = 0.0;
@@ -836,6 +852,7 @@ static int solve_qp_impl(int n, const double *H, const double *f, int mA, const 
     C.b = malloc(sizeof(double) * (mmax + 1));
     C.is_eq = malloc(sizeof(int) * (mmax + 1));
     C.src = malloc(sizeof(int) * (mmax + 1));
+    C.qsel = nfric > 0 && fric->contact_mask != 0;
     double *full = malloc(sizeof(double) * n);
 #define ADD_CONS(normal_full, bval, eqflag, srcid)                                          \
     do {                                                                                    \
@@ -856,6 +873,11 @@ static int solve_qp_impl(int n, const double *H, const double *f, int mA, const 
 
     for (int a = 0; a < nf; ++a)
         if (lb && lb[fid[a]] > -ORC_INFTY) {
+            if (nfric && fric->elide_fz && lb[fid[a]] <= 0.0) {
+                const int k = fid[a] / fric->nu, c = fid[a] % fric->nu;
+                if (c % 3 == 2 && c / 3 < fric->nfeet && ((fric->contact_mask >> (2 * k + c / 3)) & 1ull))
+                    continue; /* implied by the foot's pyramid rows */
+            }
             memset(full, 0, sizeof(double) * n);
             full[fid[a]] = 1.0;
             ADD_CONS(full, lb[fid[a]], 0, a);
@@ -1059,7 +1081,7 @@ static int srbm_one(const orc_srbm_cfg *cfg, const double *x0, const double *xre
     orc_build_qp(nx, nu, N, Ad, Bd, cfg->Q, cfg->R, cfg->P, NULL, NULL, 0, 0, x0, xref, H, f,
                  NULL, NULL, NULL, NULL, NULL, NULL, NULL);
     orc_srbm_bounds(cfg, contact, lb, ub);
-    orc_friction fr = {cfg->friction && cfg->model == 0, nu, N, 2, cfg->mu, contact};
+    orc_friction fr = {cfg->friction && cfg->model == 0, nu, N, 2, cfg->mu, contact, cfg->elide_fz};
     int nfree = 0;
     for (int v = 0; v < nV; ++v) nfree += lb[v] != ub[v];
     const int wg = nfree > cfg->crash_split;

@@ -74,6 +74,8 @@ typedef struct {
     int nfeet;       /* 2 */
     double mu;       /* friction coefficient */
     uint64_t contact_mask;
+    int elide_fz;    /* leave out the lower bound fz >= lb (lb <= 0) of a foot in contact: its
+                        pyramid implies fz >= 0 (same feasible set; the library does the same) */
 } orc_friction;
 
 int orc_solve_qp(int n, const double *H, const double *f, int mA, const double *A,
@@ -114,6 +116,7 @@ typedef struct {
      * 0 = off (plain Goldfarb-Idnani, the solve every other path runs).  Instances with more
      * than crash_split free variables are the workgroup solver's: crash_kmax_wg / _pmax_wg. */
     int crash_kmax, crash_pmax, crash_kmax_wg, crash_pmax_wg, crash_split;
+    int elide_fz; /* orc_friction::elide_fz for the friction configurations */
 } orc_srbm_cfg;
 
 /* x0: [B][nx]; xref: [B][N+1][nx]; lin: [B][8]; contact: [B]; U: [B][nu*N] */

@@ -25,7 +25,7 @@ _up = np.ctypeslib.ndpointer(dtype=np.uint64, flags="C_CONTIGUOUS")
 
 class Friction(C.Structure):
     _fields_ = [("enabled", C.c_int), ("nu", C.c_int), ("N", C.c_int), ("nfeet", C.c_int),
-                ("mu", C.c_double), ("contact_mask", C.c_uint64)]
+                ("mu", C.c_double), ("contact_mask", C.c_uint64), ("elide_fz", C.c_int)]
 
 
 class SrbmCfg(C.Structure):
@@ -36,7 +36,7 @@ class SrbmCfg(C.Structure):
                 ("u_max", C.c_double), ("Q", C.c_void_p), ("R", C.c_void_p),
                 ("P", C.c_void_p), ("max_iter", C.c_int), ("crash_kmax", C.c_int),
                 ("crash_pmax", C.c_int), ("crash_kmax_wg", C.c_int), ("crash_pmax_wg", C.c_int),
-                ("crash_split", C.c_int)]
+                ("crash_split", C.c_int), ("elide_fz", C.c_int)]
 
 
 def crash_params(p):
@@ -169,7 +169,8 @@ def solve_qp(H, f, lb=None, ub=None, A=None, lbA=None, ubA=None, friction=None, 
     fr = None
     if friction is not None:
         fr = Friction(1, friction["nu"], friction["N"], friction.get("nfeet", 2),
-                      friction["mu"], int(friction["contact_mask"]))
+                      friction["mu"], int(friction["contact_mask"]),
+                      int(friction.get("elide_fz", 0)))
     st = lib().orc_solve_qp(n, _f(H), np.ascontiguousarray(np.asarray(f, float)), mA, _ptr(Arm),
                             0, _ptr(lb_), _ptr(ub_), _ptr(lbA_), _ptr(ubA_),
                             None if fr is None else C.cast(C.pointer(fr), C.c_void_p),
@@ -212,6 +213,10 @@ def make_cfg(p):
     cfg.max_iter = p.get("max_iter", 0)
     (cfg.crash_kmax, cfg.crash_pmax, cfg.crash_kmax_wg, cfg.crash_pmax_wg,
      cfg.crash_split) = crash_params(p)
+    # the library leaves out each contact foot's fz >= fz_min (<= 0) bound, which its friction
+    # pyramid implies (gi_setup, gi_solver.hpp); p["elide_fz"] = 0 keeps it (same minimiser,
+    # more dual passes)
+    cfg.elide_fz = int(p.get("elide_fz", 1))
     return cfg, keep
 
 

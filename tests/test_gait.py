@@ -193,7 +193,10 @@ def test_rollout_warm_start_matches_oracle_and_saves_passes(gpu, orc):
     """Warm start of the closed loop (mpcqp_set_warm_start) at config C:
     every tick's plans equal the oracle's cold solve of the same inputs (unique optimum), the
     first tick is cold (identical iteration count), and the warm ticks take fewer dual passes
-    than the cold loop over the same ticks (tools/warm_start_ab.py: up to 53 % fewer)."""
+    than the cold loop over the same ticks (tools/warm_start_ab.py: up to 53 % fewer with every
+    contact foot's fz >= 0 bound in the set; since that bound is left out -- its pyramid implies
+    it, gi_setup -- the cold loop needs ~45 % fewer passes itself and warm saves ~6 % more
+    here: 5,824 vs 6,224 passes over ticks 1-7)."""
     import mpcqp
     p = mpcqp.model_params("C")
     S, Cc, K = 32, 8, 8
@@ -201,7 +204,7 @@ def test_rollout_warm_start_matches_oracle_and_saves_passes(gpu, orc):
     warm = _closed_loop_iters(p, g, K, True, orc)
     cold = _closed_loop_iters(p, g, K, False)
     assert warm[0] == cold[0]
-    assert warm[1:].sum() < 0.9 * cold[1:].sum(), (warm, cold)
+    assert warm[1:].sum() < 0.97 * cold[1:].sum(), (warm, cold)
 
 
 @pytest.mark.gpu
