@@ -34,6 +34,7 @@ struct FastKernels {
     size_t dense_lds = 0;
     int dense_threads = 0;
     const void *disc = nullptr, *cs = nullptr, *mpc = nullptr;
+    const void *mpc_list = nullptr;  // k_mpc on the overflow list (SRBM): the paired kernel's overflow
     size_t disc_lds = 0, cs_lds = 0, mpc_lds = 0;
     int nx = 0, nu = 0;
     int prim_nf = 0;  // free variables the one-wave kernel holds (kPairCap or its NF)
@@ -81,6 +82,34 @@ __global__ void __launch_bounds__(64, (NF <= 32 ? MPCQP_W32 : MPCQP_W64)) k_mpc(
     fast_mpc<NU, N, MODEL, FRIC, NF>(a, smem_m);
 }
 
+// the overflow list's one-QP-per-wave kernel (instances the paired kernel defers: more than its
+// 30 free forces per half, at most NF): the same fused step as k_mpc on the listed instances,
+// a resident grid striding over the list; re-arms the other list and, in the fused selection,
+// commits each workgroup's minimum key and finalizes the record (as wg_mpc_grid, mpc_wg.hpp)
+template <int NU, int N, int MODEL, bool FRIC, int NF>
+__global__ void __launch_bounds__(64, (NF <= 32 ? MPCQP_W32 : MPCQP_W64))
+    k_mpc_list(MpcArgs a, int *list, int *rearm) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem_l[];
+    if (blockIdx.x == 0 && threadIdx.x < kListSubs)
+        __hip_atomic_store(&rearm[threadIdx.x * kListStride], 0, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    const OvfView ov = ovf_view(list, a.ovf_cap);
+    const int count = ov.total;
+    unsigned long long kmin = kSelNone;
+    for (int i = blockIdx.x; i < count; i += gridDim.x) {
+        unsigned long long k = kSelNone;
+        fast_mpc<NU, N, MODEL, FRIC, NF>(a, smem_l, ov.id(i), &k);
+        kmin = k < kmin ? k : kmin;
+        wave_sync();
+    }
+    if (a.sel) {
+        const int groups = count <= 0 ? 1 : (count < (int)gridDim.x ? count : (int)gridDim.x);
+        if ((int)blockIdx.x >= groups) return;
+        sel_commit(a, kmin, NU * N, (int)blockIdx.x < count,
+                   reinterpret_cast<unsigned long long *>(smem_l), groups, count <= 0);
+    }
+}
+
 // device-generated inputs: the same fused step, x0/xref/lin/contact
 // built on chip from per-state data, gait candidates and commands
 template <int NU, int N, int MODEL, bool FRIC, int NF>
@@ -100,7 +129,10 @@ FastKernels make_fast() {
     k.disc_lds = sizeof(double) * disc_lds_doubles<NX, NU>();
     k.cs_lds = CSLayout<NX, NU, N, FRIC, NFMAX>::lds_bytes;
     k.mpc = (const void *)&k_mpc<NU, N, MODEL, FRIC, NFMAX>;
-    if constexpr (MODEL == 0) k.mpc_gen = (const void *)&k_mpc_gen<NU, N, MODEL, FRIC, NFMAX>;
+    if constexpr (MODEL == 0) {
+        k.mpc_gen = (const void *)&k_mpc_gen<NU, N, MODEL, FRIC, NFMAX>;
+        k.mpc_list = (const void *)&k_mpc_list<NU, N, MODEL, FRIC, NFMAX>;
+    }
     k.mpc_lds = MpcLayout<NU, N, FRIC, NFMAX>::lds_bytes;
     k.nx = NX;
     k.nu = NU;

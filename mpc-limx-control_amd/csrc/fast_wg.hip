@@ -7,6 +7,10 @@
 #include "fast_kernels.hpp"
 #include "mpc_wg.hpp"
 
+#ifndef MPCQP_OVF_ONEWAVE
+#define MPCQP_OVF_ONEWAVE 1
+#endif
+
 namespace mpcqp {
 namespace {
 
@@ -37,6 +41,16 @@ bool add_fast_wg(int model, int N, bool fric, FastKernels &k) {
     const bool crash = !fric && MPCQP_WG_SRBM_CRASH;
     k.crash_k_wg = crash ? kWgCrashK : 0;
     k.crash_p_wg = crash ? kWgCrashP : 0;
+    // N = 10 behind the paired kernel: at most 6N = 60 free forces, which the one-QP-per-wave
+    // k_mpc<.., 64> holds -- its list form takes the overflow (MPCQP_OVF_ONEWAVE);
+    // 0: the workgroup kernel (A/B builds)
+    if (N == 10 && MPCQP_OVF_ONEWAVE && k.pair && k.mpc_list && k.nf >= 6 * N) {
+        k.wg = k.mpc_list;
+        k.wg_lds = k.mpc_lds;
+        k.wg_threads = 64;
+        k.crash_k_wg = k.crash_p_wg = 0;
+        return true;
+    }
     if (N == 10) { fric ? add_wg<10, true, 64>(k) : add_wg<10, false, 64>(k); return true; }
     if (N == 20) { fric ? add_wg<20, true, 128>(k) : add_wg<20, false, 128>(k); return true; }
     return false;

@@ -347,7 +347,7 @@ __device__ __forceinline__ bool wg_crash(GiCtx &C, const double (&Jr)[NF / 2], d
 template <int NF, bool CRASH = false>
 __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double g, double *W) {
     using Lay = WgLayout<NF>;
-    constexpr int NH = Lay::NH, CBW = Lay::CBW, RW = Lay::RW, NWH = WgShape<NF>::NWH;
+    constexpr int NH = Lay::NH, RW = Lay::RW, NWH = WgShape<NF>::NWH;
     constexpr bool TWO = RW > 64;  // wave 0 keeps two slots per lane (ln, ln + 64)
     GiLds &L = C.L;
     const SolveProblem &P = *C.P;

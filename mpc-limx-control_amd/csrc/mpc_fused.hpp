@@ -158,7 +158,6 @@ __device__ __forceinline__ void sel_final_reduce(const MpcArgs &a, int nV,
 __device__ __forceinline__ void sel_commit_t(const MpcArgs &a, unsigned long long k, int nV,
                                              bool wrote, unsigned long long *scratch, int groups,
                                              int tid, bool fresh = false) {
-    const int nt = (int)blockDim.x;
     int &sel_last = *reinterpret_cast<int *>(scratch + 16);
     unsigned long long *sel_red = scratch;
     unsigned long long *slot = &a.sel[(blockIdx.x % kSelSlots) * kSelStride];
@@ -541,16 +540,21 @@ __device__ __forceinline__ double mpc_g_entry(const double *D, int vi) {
     return 2.0 * s;
 }
 
+// b_in < 0: instance xcd_order(blockIdx.x) of the batch, deferred to the overflow list when its
+// free forces exceed NF, its key committed to the fused selection here.  b_in >= 0 (the
+// overflow list's one-wave kernel, k_mpc_list): that instance, never deferred (more than NF
+// free forces: ST_BAD_DIMS), its selection key returned in *key_out instead of committed.
 template <int NU, int N, int MODEL, bool FRIC, int NF, bool GEN = false>
-__device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) {
+__device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem, int b_in = -1,
+                                         unsigned long long *key_out = nullptr) {
     static_assert(!GEN || MODEL == 0, "generated inputs are defined for the SRBM model");
     using Lay = MpcLayout<NU, N, FRIC, NF>;
     constexpr int NX = 13, NS = NX + NU, NV = Lay::NV, LD = Lay::LD;
-    const int b = xcd_order((int)blockIdx.x, (int)gridDim.x), ln = lane();
+    const bool listed = b_in >= 0;
+    const int b = listed ? b_in : xcd_order((int)blockIdx.x, (int)gridDim.x), ln = lane();
     double *D = reinterpret_cast<double *>(smem);
-    double *X0 = D + Lay::oX0, *X1 = D + Lay::oX1, *S = D + Lay::oS, *UV = D + Lay::oUV;
+    double *S = D + Lay::oS, *UV = D + Lay::oUV;
     static_assert(MODEL == 0 || MODEL == 1, "TRON1 models only");
-    double *Ax = D + Lay::oAx, *A2x = Ax + NX;
     MPCQP_STAMP_INIT(tst);
 
     // ---- solver context (bounds from the contact schedule)
@@ -593,9 +597,9 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     // the free map first (it reads only the bounds and the contact schedule): an instance the
     // workgroup kernel takes returns before the model terms
     gi_setup(C);  // free map + constraint states
-    if (C.nf > a.max_free) C.status = ST_BAD_DIMS;
+    if (C.nf > a.max_free || (listed && C.nf > NF)) C.status = ST_BAD_DIMS;
     wave_sync();
-    if (a.ovf && C.nf > NF && C.nf <= a.max_free) {  // the workgroup kernel takes it
+    if (!listed && a.ovf && C.nf > NF && C.nf <= a.max_free) {  // the overflow kernel takes it
         if (ln == 0) wg_list_append(a.ovf, a.ovf_cap, b, true, 0, false);
         return;
     }
@@ -611,19 +615,6 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     // ---- H_FF (lane p builds row p) and g
     const int nf = C.nf;
     const bool ok = C.status == ST_OK && nf > 0;
-    auto H_entry = [&](int vi, int vj) -> double {
-        const int ki = vi / NU, ci = vi % NU, kj = vj / NU, cj = vj % NU;
-        const int kk = ki > kj ? ki : kj;
-        double c, si, sj, sij;
-        beta_sums(kk + 1, N - 1, ki, kj, c, si, sj, sij);
-        const double bi = (double)(N - 1 - ki) + 0.5, bj = (double)(N - 1 - kj) + 0.5;
-        const double *So = S + (cj * NU + ci) * 4;  // cross blocks are zero (XSupport)
-        (void)si; (void)sj;
-        double v = c * So[0] + sij * So[1];
-        v += So[2] + bi * bj * So[3];
-        if (ki == kj) v += D[Lay::oRm + cj * NU + ci];
-        return 2.0 * v;
-    };
     double gp = 0.0;
     if (ok && ln < nf) {
         const int vi = C.L.fid[ln], ki = vi / NU, ci = vi % NU;
@@ -708,8 +699,12 @@ __device__ __forceinline__ void fast_mpc(const MpcArgs &a, unsigned char *smem) 
     gi_write(C, O);
     // (a deferred instance returned above; its key comes from the workgroup kernel, which then
     // is the finalizing launch)
-    if (a.sel) sel_commit(a, sel_key(C.status, C.fval + C.c0, a.sel_base + b), NV, true,
-                          reinterpret_cast<unsigned long long *>(D + Lay::oR));
+    if (listed) {
+        if (key_out) *key_out = sel_key(C.status, C.fval + C.c0, a.sel_base + b);
+    } else if (a.sel) {
+        sel_commit(a, sel_key(C.status, C.fval + C.c0, a.sel_base + b), NV, true,
+                   reinterpret_cast<unsigned long long *>(D + Lay::oR));
+    }
     MPCQP_STAMP(a.stamps, 9, tw);
     (void)NS;
 }

@@ -645,6 +645,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         // ---- solver (gi_run_reg with NF = 30 per half)
         constexpr bool kRinv = MPCQP_PAIR_RINV;
         double *Lc = D + Lay::oR, *R = D + Lay::oR, *Ri = D + Lay::oR;  // R (or R^-1) over dead L
+        (void)Lc;
         double *rowbuf = D + Lay::oRow, *colb = rowbuf + NP, *rot = rowbuf + 2 * NP,
                *rinv = rowbuf + 4 * NP;
         double u = 0.0;
