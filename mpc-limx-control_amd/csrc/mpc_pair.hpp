@@ -55,6 +55,11 @@ namespace mpcqp {
 #ifndef MPCQP_PAIR_FOLD
 #define MPCQP_PAIR_FOLD 1
 #endif
+// the folded sweep's rows load from a per-slot selected address (one LDS read per slot) instead
+// of reading both candidates and selecting the value (A/B)
+#ifndef MPCQP_FOLD_ASEL
+#define MPCQP_FOLD_ASEL 1
+#endif
 // the dual loop keeps R^-1 instead of R (r = R^-1 d as a lane-parallel product, no serial
 // back substitution); 0 keeps R (A/B builds)
 #ifndef MPCQP_PAIR_RINV
@@ -681,8 +686,12 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 const double *Hr = D + Lay::oR + lrow(hl), *Hc = D + Lay::oR + hl;
     #pragma unroll
                 for (int q = 0; q < NF; ++q) {
-                    const double lo_ = Hr[q], up_ = Hc[lrow(q)];  // (q, l) read for q > l
-                    Jr[q] = (q <= hl) ? lo_ : up_;
+                    if (MPCQP_FOLD_ASEL) {  // one load from the selected address
+                        Jr[q] = *((q <= hl) ? Hr + q : Hc + lrow(q));  // (q, l) read for q > l
+                    } else {
+                        const double lo_ = Hr[q], up_ = Hc[lrow(q)];  // (q, l) read for q > l
+                        Jr[q] = (q <= hl) ? lo_ : up_;
+                    }
                 }
             }
             wave_sync();

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 evidence set at the current library (GPU box, repo root), all tagged TAG:
+# Evidence set at the current library (GPU box, repo root), all tagged TAG:
 #   gpurun_out/ev_TAG/bench.json            the default bench line (cpu baseline, per-config)
 #   gpurun_out/ev_TAG/B/{trace,fetch,write} headline k_mpc_pair: kernel trace + HBM passes
 #   gpurun_out/ev_TAG/B_flops/{sq,grbm}     executed FP64 / MFMA counters of the headline
@@ -7,11 +7,12 @@
 #                                           configs C (65,536) and E (16,384), driven by
 #                                           tools/time_kernel.py: the trace's (kernel, grid) group
 #                                           is the launch per_config.kernel_ms times
-#   gpurun_out/ev_TAG/Bst/trace             k_mpc_pair + k_mpc_wg at B standing (overflow path)
-# Summaries are written on the CPU afterwards (tools/summarize_r04_evidence.sh).  Counter passes
+#   gpurun_out/ev_TAG/Bst/trace             k_mpc_pair + k_mpc_list at B standing (overflow path)
+#   gpurun_out/ev_TAG/{B,C,E}_stall          stall / issue counters (tools/pmc_stall.sh)
+# Summaries are written on the CPU afterwards (tools/summarize_evidence.sh).  Counter passes
 # never share a run with trace domains.
 set -o pipefail
-TAG=${1:-r04}
+TAG=${1:-r05}
 O=gpurun_out/ev_$TAG
 mkdir -p $O
 export TMPDIR=/tmp
@@ -36,5 +37,8 @@ for spec in "C:--configs C --batch 65536" "E:--configs E --batch 16384"; do
   run ${c}_write 200 rocprofv3 --pmc WRITE_SIZE -d $R/$O/$c/write -o run --output-format csv -- python3 tools/time_kernel.py $a --reps 5
   run ${c}_flops 400 bash tools/pmc_flops.sh $O/${c}_flops --driver "tools/time_kernel.py $a --reps 5"
 done
+run B_stall 400 bash tools/pmc_stall.sh $O/B_stall
+run C_stall 400 bash tools/pmc_stall.sh $O/C_stall --driver "tools/time_kernel.py --configs C --batch 65536 --reps 5"
+run E_stall 400 bash tools/pmc_stall.sh $O/E_stall --driver "tools/time_kernel.py --configs E --batch 16384 --reps 5"
 run Bst_trace 300 rocprofv3 --kernel-trace --stats -d $R/$O/Bst/trace -o run --output-format csv -- python3 tools/time_kernel.py --configs B --gait standing --reps 10
 echo "evidence $TAG OK"

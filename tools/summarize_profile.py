@@ -36,7 +36,11 @@ def counter(path, kernel, grid):
 
 
 def lib_build_id():
-    """source hash compiled into the library that was profiled (mpcqp_build_id)"""
+    """source hash compiled into the library that was profiled (mpcqp_build_id): the one the GPU
+    run recorded (MPCQP_PROFILED_BUILD_ID, set by tools/summarize_evidence.sh from the run's bench
+    line), else the in-tree library's"""
+    if os.environ.get("MPCQP_PROFILED_BUILD_ID"):
+        return os.environ["MPCQP_PROFILED_BUILD_ID"]
     try:
         import ctypes
         L = ctypes.CDLL(os.path.join(ROOT, "mpc-limx-control_amd", "lib", "libmpcqp.so"))

@@ -10,6 +10,7 @@ import glob
 import json
 import os
 import statistics as st
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -33,7 +34,9 @@ def main():
             if tag(r["Kernel_Name"]) == a.kernel and int(r["Grid_Size"]) == a.grid:
                 vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
     c = {k: st.median(v) for k, v in vals.items()}
-    out = dict(tag=a.tag, kernel=a.kernel, grid=a.grid, counters=c)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from summarize_profile import lib_build_id
+    out = dict(tag=a.tag, lib_build_id=lib_build_id(), kernel=a.kernel, grid=a.grid, counters=c)
     wc = c.get("SQ_WAVE_CYCLES")
     if wc:
         out["frac_of_wave_cycles"] = {k: c[k] / wc for k in (
