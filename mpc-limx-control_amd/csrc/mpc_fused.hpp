@@ -58,7 +58,8 @@ struct MpcArgs {
     int *status, *iters;
     unsigned long long *stamps;
     // diagnostic (mpcqp_count_solver_flops): the paired kernel adds the textbook flops of its
-    // crash working-set solves and dual passes here (one atomic per wavefront); nullptr: off
+    // crash working-set solves and dual passes here (one atomic per wavefront, into slot
+    // blockIdx % kFlopsSlots: 32,768 atomics on one address serialise); nullptr: off
     double *flops_acc;
     int cut;  // diagnostic cuts build only
     // device-generated inputs (GEN kernels): instance b = state b / cands,
@@ -82,6 +83,9 @@ struct MpcArgs {
     long long *sel_rec;
     int sel_final;
 };
+
+constexpr int kFlopsSlots = 256, kFlopsStride = 16;  // flops_acc: slots 128 B apart
+constexpr int kFlopsWords = kFlopsSlots * kFlopsStride;
 
 // ---- fused selection (the record of k_select_min, mpcqp_kernels.hip, without its launch)
 constexpr unsigned long long kSelNone = 0x7fffffffffffffffull;

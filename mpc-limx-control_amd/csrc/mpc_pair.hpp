@@ -973,7 +973,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 const bool inA = solving && side != 0;
                 if (crashing && k == 0) { xc = x0v; lam = 0.0; fc = f0; }
                 if (solving) ++iters;
-                if (solving) sfl += crash_ws_flops_d(nf, k);
+                if (a.flops_acc && solving) sfl += crash_ws_flops_d(nf, k);
                 const int ks = solving ? k : 0;
                 const int kmax = max(__builtin_amdgcn_readlane(ks, 0), __builtin_amdgcn_readlane(ks, kHalf));
                 if (kmax == 0) continue;  // (wave-uniform)
@@ -1148,7 +1148,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             const bool stepping = go && !done;
             if (stepping) {
                 ++iters;
-                sfl += pass_flops_d(nf, q);
+                if (a.flops_acc) sfl += pass_flops_d(nf, q);
                 // |d(0:q)|^2 and |d(q+1:nf)|^2 in one two-sum pass; zn = |d2|^2 = zq + d_q^2 and
                 // dd = |d|^2 = zn + the first part
                 double sq = hl < q ? dj * dj : 0.0;
@@ -1445,7 +1445,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     }
     if (a.flops_acc) {  // (diagnostic) both halves' solver flops, one atomic per wavefront
         const double t = readlane(sfl, 0) + readlane(sfl, kHalf);
-        if (lno == 0) atomicAdd(a.flops_acc, t);
+        if (lno == 0) atomicAdd(a.flops_acc + (blockIdx.x % kFlopsSlots) * kFlopsStride, t);
     }
 #ifndef MPCQP_FUSED_SEL
 #define MPCQP_FUSED_SEL 1

@@ -1007,8 +1007,8 @@ int mpcqp_count_solver_flops(mpcqp_ctx *c, int on) {
     if (!c) return MPCQP_ERR_BAD_ARG;
     if (on && !c->dflops) {
         hipSetDevice(c->device);
-        if (hipMalloc(&c->dflops, sizeof(double)) != hipSuccess ||
-            hipMemset(c->dflops, 0, sizeof(double)) != hipSuccess) {
+        if (hipMalloc(&c->dflops, sizeof(double) * kFlopsWords) != hipSuccess ||
+            hipMemset(c->dflops, 0, sizeof(double) * kFlopsWords) != hipSuccess) {
             hipFree(c->dflops);
             c->dflops = nullptr;
             return MPCQP_ERR_DEVICE;
@@ -1021,12 +1021,13 @@ int mpcqp_count_solver_flops(mpcqp_ctx *c, int on) {
 double mpcqp_solver_flops(mpcqp_ctx *c, int *launches) {
     if (launches) *launches = 0;
     if (!c || !c->dflops) return -1.0;
-    double v = 0.0;
+    double h[kFlopsWords], v = 0.0;
     hipSetDevice(c->device);
     if (hipStreamSynchronize(c->stream) != hipSuccess ||
-        hipMemcpy(&v, c->dflops, sizeof(double), hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemset(c->dflops, 0, sizeof(double)) != hipSuccess)
+        hipMemcpy(h, c->dflops, sizeof h, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemset(c->dflops, 0, sizeof h) != hipSuccess)
         return -1.0;
+    for (int i = 0; i < kFlopsSlots; ++i) v += h[i * kFlopsStride];
     if (launches) *launches = c->flops_launches;
     c->flops_launches = 0;
     return v;
