@@ -60,6 +60,11 @@ namespace mpcqp {
 #ifndef MPCQP_FOLD_ASEL
 #define MPCQP_FOLD_ASEL 1
 #endif
+// the H build's sub-blocks address their entries from per-sub-block bases (compile-time offsets),
+// and g's terms are masked by an FMA with 0 / 1 instead of a value select (A/B)
+#ifndef MPCQP_HB_BASES
+#define MPCQP_HB_BASES 1
+#endif
 // the dual loop keeps R^-1 instead of R (r = R^-1 d as a lane-parallel product, no serial
 // back substitution); 0 keeps R (A/B builds)
 #ifndef MPCQP_PAIR_RINV
@@ -559,7 +564,8 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             for (int m = 1; m <= N; ++m) {  // m > ki; unrolled, branch-free: the loads issue together
                 const double beta = (double)(m - 1 - ki) + 0.5;
                 const double tm = UV[(m * 2 + 0) * NU + ci] + beta * UV[(m * 2 + 1) * NU + ci];
-                s += (m > ki) ? tm : 0.0;
+                if (MPCQP_HB_BASES) s = fma((m > ki) ? 1.0 : 0.0, tm, s);  // (exact: x 1 / x 0)
+                else s += (m > ki) ? tm : 0.0;
             }
             gp = 2.0 * s;
         }
@@ -605,6 +611,37 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                     nI += p_i >= 0 ? 1 : 0;
                     nJ += p_j >= 0 ? 1 : 0;
                 }
+#if MPCQP_HB_BASES
+                // per sub-block: the S / R entry base and the three packed-row bases of H_FF;
+                // the 3x3 entries then sit at compile-time offsets from them.  Positions ascend
+                // with the slot (a triple per slot), so in a diagonal block (ki == kj) slot
+                // pairs ta < tb are strictly upper (skipped), ta > tb strictly lower, and
+                // ta == tb keeps a3 >= b3 (the others go to the dump slot, branch-free)
+                const bool diag = ki == kj;
+    #pragma unroll
+                for (int ta = 0; ta < NFT; ++ta) {
+    #pragma unroll
+                    for (int tb = 0; tb < NFT; ++tb) {
+                        if (pI[ta] < 0 || pJ[tb] < 0 || (ta < tb && diag)) continue;
+                        const int sb = 3 * fJ[tb] * NU + 3 * fI[ta];
+                        const double *Sb = S + sb * 4, *Rb = Rm + sb;
+                        const int h0 = lrow(pI[ta]) + pJ[tb];
+                        const int hrow[3] = {h0, h0 + pI[ta] + 1, h0 + 2 * pI[ta] + 3};
+    #pragma unroll
+                        for (int a3 = 0; a3 < 3; ++a3) {
+    #pragma unroll
+                            for (int b3 = 0; b3 < 3; ++b3) {
+                                const double *So = Sb + (b3 * NU + a3) * 4;
+                                double v = c * So[0] + sij * So[1];
+                                v += So[2] + bij * So[3];
+                                v = fma(rf, Rb[b3 * NU + a3], v);
+                                const bool dump = ta == tb && a3 < b3 && diag;
+                                Hb[dump ? Lay::oDump - Lay::oR : hrow[a3] + b3] = 2.0 * v;
+                            }
+                        }
+                    }
+                }
+#else
     #pragma unroll
                 for (int ta = 0; ta < NFT; ++ta) {
     #pragma unroll
@@ -627,6 +664,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                         }
                     }
                 }
+#endif
             }
         }
         // rows without a free variable (past nf, or a half with nothing to solve) are identity
