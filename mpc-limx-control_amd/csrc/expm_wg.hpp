@@ -234,6 +234,11 @@ __device__ __forceinline__ void wg_pade_solve(int nx, int ns, const double *U, c
 // the columns left of k are never read again (their entries are garbage afterwards), and each
 // lane keeps its own pivot D(j, j) in a register from its step on.  The numerator columns
 // (j >= nx > k) get exactly the same operations, so E is bit-identical.
+// MPCQP_PADE_LATE: column k is read row by row in the update (after the swap) instead of 2 NXC
+// v_readlane up front, whose 48 SGPR results per step the compiler hoisted together (A/B)
+#ifndef MPCQP_PADE_LATE
+#define MPCQP_PADE_LATE 1
+#endif
 #ifndef MPCQP_PADE_NOSEL
 #define MPCQP_PADE_NOSEL 1
 #endif
@@ -276,7 +281,11 @@ __device__ __forceinline__ void wave_pade_gj(int ns, const double *U, const doub
         }
         const int p = __builtin_amdgcn_readlane(ti[0], k);
         double ck[NXC];  // column k before the swap, every lane
-        if (MPCQP_PADE_LDS) {
+        if (MPCQP_PADE_LATE) {
+            // (each row's column-k entry is read in the update loop below, after the swap)
+#pragma unroll
+            for (int i = 0; i < NXC; ++i) ck[i] = 0.0;
+        } else if (MPCQP_PADE_LDS) {
             if (j == k) {
 #pragma unroll
                 for (int i = 0; i < NXC; ++i) scr[i] = a[i];
@@ -312,12 +321,15 @@ __device__ __forceinline__ void wave_pade_gj(int ns, const double *U, const doub
             default: break;
         }
         a[k] = pk;  // ckk = piv
+        if (MPCQP_PADE_LATE) ckk = readlane(pk, k);  // D(p, k)
         if (MPCQP_PADE_NOSEL) piv_own = (j == k) ? pk : piv_own;
         const double rp = 1.0 / ckk;
 #pragma unroll
         for (int i = 0; i < NXC; ++i) {
             if (i == k) continue;
-            const double ci = (i > k && p == i) ? ck[k] : ck[i];  // row i's column-k entry after the swap
+            // row i's column-k entry after the swap (MPCQP_PADE_LATE: read from the row itself,
+            // which the swap already placed; one short SGPR live range per row)
+            const double ci = MPCQP_PADE_LATE ? readlane(a[i], k) : (i > k && p == i) ? ck[k] : ck[i];
             if (MPCQP_PADE_NOSEL) {
                 a[i] = a[i] - (ci * rp) * pk;
             } else {

@@ -7,7 +7,8 @@
 R=$(cd "$(dirname "$0")/.." && pwd)
 TU=${TU:-fast_pair}
 cd "$R/mpc-limx-control_amd" || exit 1
-HF="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -w -mllvm -pragma-unroll-threshold=1000000 -mllvm -amdgpu-sched-strategy=max-ilp"
+HF="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -w -mllvm -pragma-unroll-threshold=1000000"
+[ -n "$NOILP" ] || HF="$HF -mllvm -amdgpu-sched-strategy=max-ilp"  # NOILP=1: the default scheduler
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   # the variant's flags go into mpcqp_build_id() (PMC summaries of variants stay distinct)
