@@ -557,9 +557,9 @@ def test_overflow_workgroup_kernel_vs_oracle(gpu, orc, config, B):
     whatever the bounds, src/QPSolver.cpp:87-96): alternating, double-support and standing
     candidates (gait "mixed") plus random extra double-support and flight steps.  Instances
     beyond the one-wave kernel's capacity (30 free forces for the paired kernel at N = 10, 64
-    for k_mpc at N = 20) go through the overflow list to the 4-wave workgroup kernel (up to 6N
-    = 60 / 120 free forces); every instance is written exactly once (sentinel pre-fill) and
-    matches the oracle."""
+    for k_mpc at N = 20) go through the overflow list: at N = 10 to the one-QP-per-wave
+    k_mpc_list (up to 6N = 60 free forces), at N = 20 to the 4-wave workgroup kernel (up to
+    120); every instance is written exactly once (sentinel pre-fill) and matches the oracle."""
     import mpcqp
     from mpcqp.engine import BatchEngine
     p = mpcqp.model_params(config)
