@@ -9,7 +9,7 @@ and the mean / max solver passes.  With MPCQP_LIB pointing at libmpcqp_stamps.so
 prints the per-WAVE cycles of each phase (s_memtime, summed over the wave's phases), which at
 small batches is the latency of a lone wavefront.
 
-  python tools/r03_sweep.py [--sizes 512,4096,8192] [--max-free 30] [--reps 50]
+  python tools/shard_sweep.py [--sizes 512,4096,8192] [--max-free 30] [--reps 50]
 """
 import argparse
 import ctypes as C

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """profiles/pmc_traffic_<config>.json from a FETCH_SIZE / WRITE_SIZE pass pair (tools/ab_traffic.sh
-or tools/r02_pmc_cfg.sh layout: DIR/{FETCH_SIZE,WRITE_SIZE}/run_counter_collection.csv), for one
+or the evidence.sh layout: DIR/{FETCH_SIZE,WRITE_SIZE}/run_counter_collection.csv), for one
 kernel instantiation at one grid size.  reads = 2 x FETCH_SIZE (gfx950 half count), writes =
 WRITE_SIZE, KiB.  bench.py's per_config lines report it beside the algorithmic bytes.
 Usage: tools/summarize_traffic.py DIR TAG --config C --batch 65536 --kernel 'k_mpc<6, 20, 0, true, 60>' --grid 4194304"""
