@@ -11,7 +11,7 @@
 #   NOILP=1 [TU=...] tools/build_variants.sh noilp_b: / noilp_c: / noilp_e:
 #   [TU=...] tools/build_variants.sh sb_<s>:"-mllvm -amdgpu-sched-strategy=<s>" (sc_ / se_ likewise)
 # (the flags' current defaults are the kept side; variants whose code was removed after a
-#  negative result -- oldcrash, cpairs, pmfma, padesw_e, prio1 / prio2 / prio_e / prio_w -- are in git history)
+#  negative result -- oldcrash, cpairs, pmfma, rpnew / rpasel, padesw_e, prio1 / prio2 / prio_e / prio_w -- are in git history)
 set -o pipefail
 NAME=${1:?usage: tools/runs.sh <name> [tag]}
 T=${2:-$NAME}
@@ -81,5 +81,6 @@ case "$NAME" in
   hb-bases)    log rep 3 ab_b hbbases && pair_tests hbbases ;;  # H-build sub-block bases
   crash-pairs) log rep 3 ab_b cpairs && pair_tests cpairs ;;    # crash Gram by entry pairs
   pair-mfma)   pair_tests pmfma && log rep 3 ab_b pmfma ;;      # paired factorisation on MFMA
+  rowpair)     pair_tests rpnew && log rep 3 ab_b rpnew rpasel ;;  # DPP64 broadcasts, lane-mask selects
   *) echo "unknown run: $NAME" >&2; exit 2 ;;
 esac
