@@ -11,7 +11,7 @@
 #   NOILP=1 [TU=...] tools/build_variants.sh noilp_b: / noilp_c: / noilp_e:
 #   [TU=...] tools/build_variants.sh sb_<s>:"-mllvm -amdgpu-sched-strategy=<s>" (sc_ / se_ likewise)
 # (the flags' current defaults are the kept side; variants whose code was removed after a
-#  negative result -- oldcrash, cpairs, pmfma, rpnew / rpasel, padesw_e, prio1 / prio2 / prio_e / prio_w -- are in git history)
+#  negative result -- oldcrash, cpairs, pmfma, rpnew / rpasel, gj2, padesw_e, prio1 / prio2 / prio_e / prio_w -- are in git history)
 set -o pipefail
 NAME=${1:?usage: tools/runs.sh <name> [tag]}
 T=${2:-$NAME}
@@ -82,5 +82,7 @@ case "$NAME" in
   crash-pairs) log rep 3 ab_b cpairs && pair_tests cpairs ;;    # crash Gram by entry pairs
   pair-mfma)   pair_tests pmfma && log rep 3 ab_b pmfma ;;      # paired factorisation on MFMA
   rowpair)     pair_tests rpnew && log rep 3 ab_b rpnew rpasel ;;  # DPP64 broadcasts, lane-mask selects
+  crash-gj2)   timeout -k 10 300 python3 tools/cmp_libs.py mpc-limx-control_amd/lib/libmpcqp.so mpc-limx-control_amd/lib/libmpcqp_gj2.so &&
+               log rep 3 ab_b gj2 ;;                   # crash Gauss-Jordan, two pivots per round trip
   *) echo "unknown run: $NAME" >&2; exit 2 ;;
 esac
