@@ -30,6 +30,9 @@ for i in range(B):
     x0 = -J @ (J.T @ g)
     probs.append((J, x0, lb[F], ub[F]))
 
+ADD_ONLY = [0, 0, 0, 0]  # later sets that only append, all later sets, their rows, all rows
+
+
 def crash(J, x0, lo, hi, rule, kmax=12, pmax=8):
     n = len(x0); side = np.zeros(n, int); lam = np.zeros(n); xc = x0.copy()
     sets = []
@@ -65,6 +68,13 @@ def crash(J, x0, lo, hi, rule, kmax=12, pmax=8):
                 if side[j] == 0 and nw[j] != 0:
                     if room > 0: room -= 1
                     else: nw[j] = 0
+        if rule == ("none",) and it > 0 and (side != 0).any():
+            drops = ((side != 0) & (nw == 0)).any()
+            ADD_ONLY[0] += not drops
+            ADD_ONLY[1] += 1
+            ADD_ONLY[2] += (nw != 0).sum() if not drops else 0
+        if rule == ("none",):
+            ADD_ONLY[3] += (nw != 0).sum()
         side = nw; it += 1
         A = np.flatnonzero(side)
         if len(A) == 0: xc = x0.copy(); lam[:] = 0; continue
@@ -93,4 +103,6 @@ for rule in rules:
     if rule == ("none",):
         it = o["iters"]
         print("   oracle iters == sets:", np.mean(it == nsets))
+print(f"kept rule: {ADD_ONLY[0]} of {ADD_ONLY[1]} later sets only append bounds; their rows "
+      f"are {ADD_ONLY[2]} of the {ADD_ONLY[3]} rows solved")
 print("%.1fs" % (time.time()-t0))
