@@ -11,7 +11,7 @@
 #   NOILP=1 [TU=...] tools/build_variants.sh noilp_b: / noilp_c: / noilp_e:
 #   [TU=...] tools/build_variants.sh sb_<s>:"-mllvm -amdgpu-sched-strategy=<s>" (sc_ / se_ likewise)
 # (the flags' current defaults are the kept side; variants whose code was removed after a
-#  negative result -- oldcrash, cpairs, pmfma, rpnew / rpasel, gj2, padesw_e, prio1 / prio2 / prio_e / prio_w -- are in git history)
+#  negative result -- oldcrash, cpairs, pmfma, rpnew / rpasel, gj2, inc / kc10, padesw_e, prio1 / prio2 / prio_e / prio_w -- are in git history)
 set -o pipefail
 NAME=${1:?usage: tools/runs.sh <name> [tag]}
 T=${2:-$NAME}
