@@ -300,11 +300,12 @@ __device__ __forceinline__ void gi_setup(GiCtx &C) {
             var_bounds(P, v, lo, hi);
             s = (id < nf) ? (lo > -kInfty ? 1 : 0) : (hi < kInfty ? 1 : 0);
             // the lower bound fz >= lo <= 0 of a foot in contact is implied by its friction
-            // pyramid (mu fz -+ fx >= 0 sum to fz >= 0): left out, the same feasible set and
+            // pyramid (mu fz -+ fx >= 0 sum to fz >= 0 when mu > 0; at mu = 0 the rows only pin
+            // fx, fy and the bound stays): left out, the same feasible set and
             // minimiser without the degenerate apex where five constraints meet in 3-D (the
             // dual loop's add / drop cycles there: config C's mean passes 5.9 -> 2.8 in the
             // oracle); the oracle does the same (orc_friction::elide_fz)
-            if (MPCQP_ELIDE_FZ && id < nf && nfric > 0 && s == 1 && lo <= 0.0) {
+            if (MPCQP_ELIDE_FZ && id < nf && nfric > 0 && s == 1 && lo <= 0.0 && P.mu > 0.0) {
                 const int k = v / P.nu, c = v % P.nu;
                 if (c % 3 == 2 && c / 3 < P.nfeet && ((P.contact >> (2 * k + c / 3)) & 1ull)) s = 0;
             }

@@ -873,7 +873,7 @@ static int solve_qp_impl(int n, const double *H, const double *f, int mA, const 
 
     for (int a = 0; a < nf; ++a)
         if (lb && lb[fid[a]] > -ORC_INFTY) {
-            if (nfric && fric->elide_fz && lb[fid[a]] <= 0.0) {
+            if (nfric && fric->elide_fz && fric->mu > 0.0 && lb[fid[a]] <= 0.0) {
                 const int k = fid[a] / fric->nu, c = fid[a] % fric->nu;
                 if (c % 3 == 2 && c / 3 < fric->nfeet && ((fric->contact_mask >> (2 * k + c / 3)) & 1ull))
                     continue; /* implied by the foot's pyramid rows */

@@ -75,3 +75,30 @@ def test_fuzz_params_vs_oracle(gpu, orc, seed):
     np.testing.assert_allclose(o["cost"][ok], ref["cost"][ok], rtol=1e-9, atol=1e-9,
                                err_msg=str(tag))
     assert np.mean(o["iters"][ok] == ref["iters"][ok]) >= 0.95, tag
+
+
+def test_zero_friction_coefficient_vs_oracle(gpu, orc):
+    """mu = 0: the friction rows pin fx, fy only, so the fz lower bound must stay in the problem
+    (the implied-bound elision requires mu > 0); with the body moving up the unconstrained
+    optimum pulls it down, and the solvers must still return fz >= fz_min"""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("C")
+    p["mu"] = 0.0
+    batch = mpcqp.make_batch(p, 256, seed=9001)
+    batch["x0"][:, 11] = 3.0
+    eng = BatchEngine(p)
+    d = eng.upload(batch)
+    eng.solve(d)
+    eng.sync()
+    o = {k: d[k].cpu().numpy() for k in ("U", "cost", "status", "iters")}
+    eng.close()
+    ref = orc.srbm_batch(p, batch["x0"], batch["xref"], batch["lin"], batch["contact"])
+    np.testing.assert_array_equal(o["status"], ref["status"])
+    assert np.all(o["status"] == 0)
+    fz = o["U"].reshape(len(o["U"]), p["N"], 2, 3)[..., 2]
+    assert fz.min() >= p["fz_min"] - 1e-8
+    for i in range(len(o["U"])):
+        scale = max(1.0, np.abs(ref["U"][i]).max())
+        assert np.abs(o["U"][i] - ref["U"][i]).max() <= TOL_U * scale, i
+    np.testing.assert_allclose(o["cost"], ref["cost"], rtol=1e-9, atol=1e-9)

@@ -59,3 +59,21 @@ def test_tie_stable_selection_under_perturbation(orc):
     x0 = batch["x0"] * (1.0 + 1e-11 * np.random.default_rng(5).standard_normal(batch["x0"].shape))
     b = orc.srbm_batch(p, x0, batch["xref"], batch["lin"], batch["contact"], nthreads=4)
     assert np.mean(a["iters"] == b["iters"]) >= 0.999
+
+
+def test_elide_fz_needs_a_positive_friction_coefficient(orc):
+    """at mu = 0 the pyramid rows only pin fx, fy (mu fz -+ fx >= 0 no longer sums to fz >= 0),
+    so the fz lower bound is kept: a body moving up (the optimum pulls it down) still gets
+    fz >= fz_min, and the elision flag changes nothing"""
+    p = mpcqp.model_params("C")
+    p["mu"] = 0.0
+    batch = mpcqp.make_batch(p, 256, seed=83)
+    batch["x0"][:, 11] = 3.0  # v_z up
+    args = (batch["x0"], batch["xref"], batch["lin"], batch["contact"])
+    plain = orc.srbm_batch(dict(p, elide_fz=0), *args, nthreads=4)
+    el = orc.srbm_batch(dict(p, elide_fz=1), *args, nthreads=4)
+    assert np.all(plain["status"] == 0) and np.all(el["status"] == 0)
+    fz = el["U"].reshape(len(el["U"]), p["N"], 2, 3)[..., 2]
+    assert fz.min() >= p["fz_min"] - 1e-8
+    assert np.all(_close(el["U"], plain["U"]))
+    np.testing.assert_array_equal(el["iters"], plain["iters"])
