@@ -102,3 +102,46 @@ def test_zero_friction_coefficient_vs_oracle(gpu, orc):
         scale = max(1.0, np.abs(ref["U"][i]).max())
         assert np.abs(o["U"][i] - ref["U"][i]).max() <= TOL_U * scale, i
     np.testing.assert_allclose(o["cost"], ref["cost"], rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fuzz_dense_vs_oracle(gpu, orc, seed):
+    """config E (the dense whole-body model: expm, Toeplitz condensing, 96-variable solve) with
+    the sampling time, torque bound and diagonal weights perturbed and odd batch sizes; U / cost
+    / status against the oracle, iteration counts with the workgroup crash caps"""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    rng = np.random.default_rng(9100 + seed)
+    p = mpcqp.model_params("E")
+    nx = p["nx"]
+    p["Ts"] *= rng.uniform(0.5, 2.0)
+    lim = p["u_max"] * rng.uniform(0.5, 2.0)
+    p["u_min"], p["u_max"] = -lim, lim
+    qd = np.diag(p["Q"]) * rng.uniform(0.3, 3.0, nx)
+    p["Q"] = np.diag(qd)
+    p["P"] = np.diag(qd * rng.uniform(3.0, 20.0))
+    p["R"] = np.asarray(p["R"], float) * rng.uniform(0.5, 2.0)
+    B = int(rng.choice([1, 7, 33, 65, 127, 191]))
+    batch = mpcqp.make_batch(p, B, seed=9200 + seed)
+    eng = BatchEngine(p)
+    crash = eng.crash
+    d = eng.upload(batch)
+    d["U"].fill_(float("nan"))
+    d["status"].fill_(99)
+    eng.solve(d)
+    eng.sync()
+    o = {k: d[k].cpu().numpy() for k in ("U", "cost", "status", "iters")}
+    eng.close()
+    q = dict(p)
+    q["crash"] = tuple(crash)
+    ref = orc.dense_batch(q, batch["x0"], batch["xref"], batch["lin"])
+    tag = (B, float(p["Ts"]), float(lim))
+    np.testing.assert_array_equal(o["status"], ref["status"], err_msg=str(tag))
+    ok = ref["status"] == 0
+    assert ok.mean() >= 0.9, tag
+    for i in np.flatnonzero(ok):
+        scale = max(1.0, np.abs(ref["U"][i]).max())
+        assert np.abs(o["U"][i] - ref["U"][i]).max() <= TOL_U * scale, (tag, i)
+    np.testing.assert_allclose(o["cost"][ok], ref["cost"][ok], rtol=1e-9, atol=1e-9,
+                               err_msg=str(tag))
+    assert np.mean(o["iters"][ok] == ref["iters"][ok]) >= 0.95, tag
