@@ -145,3 +145,33 @@ def test_fuzz_dense_vs_oracle(gpu, orc, seed):
     np.testing.assert_allclose(o["cost"][ok], ref["cost"][ok], rtol=1e-9, atol=1e-9,
                                err_msg=str(tag))
     assert np.mean(o["iters"][ok] == ref["iters"][ok]) >= 0.95, tag
+
+
+@pytest.mark.parametrize("config,max_iter", [("B", 2), ("C", 2), ("C", 4), ("L", 2), ("L", 5)])
+def test_iteration_cap_vs_oracle(gpu, orc, config, max_iter):
+    """mpcqp_model.max_iter small enough to bind: the same instances stop at the cap
+    (ST_ITER_LIMIT) in the kernels and the oracle -- the crash start's working sets count as
+    iterations and the dual loop stops once the count reaches the cap -- and the others match"""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params(config)
+    p["max_iter"] = max_iter
+    batch = mpcqp.make_batch(p, 512, seed=9300 + max_iter)
+    eng = BatchEngine(p)
+    crash = eng.crash
+    d = eng.upload(batch)
+    eng.solve(d)
+    eng.sync()
+    o = {k: d[k].cpu().numpy() for k in ("U", "cost", "status", "iters")}
+    eng.close()
+    q = dict(p)
+    q["crash"] = tuple(crash)
+    ref = orc.srbm_batch(q, batch["x0"], batch["xref"], batch["lin"], batch["contact"])
+    assert np.mean(o["status"] == ref["status"]) >= 0.99
+    both = (o["status"] == 0) & (ref["status"] == 0)
+    assert both.mean() > 0.25
+    for i in np.flatnonzero(both):
+        scale = max(1.0, np.abs(ref["U"][i]).max())
+        assert np.abs(o["U"][i] - ref["U"][i]).max() <= TOL_U * scale, i
+    if config != "B":
+        assert np.any(ref["status"] == 3)  # the cap binds
