@@ -175,3 +175,30 @@ def test_iteration_cap_vs_oracle(gpu, orc, config, max_iter):
         assert np.abs(o["U"][i] - ref["U"][i]).max() <= TOL_U * scale, i
     if config != "B":
         assert np.any(ref["status"] == 3)  # the cap binds
+
+
+@pytest.mark.parametrize("config,N", [("B", 5), ("B", 8), ("B", 15), ("C", 12), ("L", 6), ("L", 13)])
+def test_other_horizons_vs_oracle(gpu, orc, config, N):
+    """horizons without a compile-time kernel run the generic runtime-dimension kernels (batched
+    condensing + the one-wave solver, up to 64 free variables): U / cost / status against the
+    oracle, iteration counts equal"""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params(config, N=N)
+    if config != "L":
+        p["max_free"] = min(64, 3 * N)  # the alternating gait: one stance foot per step
+    batch = mpcqp.make_batch(p, 97, seed=9400 + N)
+    eng = BatchEngine(p)
+    d = eng.upload(batch)
+    eng.solve(d)
+    eng.sync()
+    o = {k: d[k].cpu().numpy() for k in ("U", "cost", "status", "iters")}
+    eng.close()
+    ref = orc.srbm_batch(p, batch["x0"], batch["xref"], batch["lin"], batch["contact"])
+    np.testing.assert_array_equal(o["status"], ref["status"])
+    assert np.all(o["status"] == 0)
+    for i in range(len(o["U"])):
+        scale = max(1.0, np.abs(ref["U"][i]).max())
+        assert np.abs(o["U"][i] - ref["U"][i]).max() <= TOL_U * scale, i
+    np.testing.assert_allclose(o["cost"], ref["cost"], rtol=1e-9, atol=1e-9)
+    assert np.mean(o["iters"] == ref["iters"]) >= 0.95
