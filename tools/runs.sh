@@ -84,5 +84,6 @@ case "$NAME" in
   rowpair)     pair_tests rpnew && log rep 3 ab_b rpnew rpasel ;;  # DPP64 broadcasts, lane-mask selects
   crash-gj2)   timeout -k 10 300 python3 tools/cmp_libs.py mpc-limx-control_amd/lib/libmpcqp.so mpc-limx-control_amd/lib/libmpcqp_gj2.so &&
                log rep 3 ab_b gj2 ;;                   # crash Gauss-Jordan, two pivots per round trip
+  pair-sort)   log rep 3 ab_b nosort ;;                 # schedule-sorted pairing off (nosort: -DMPCQP_PAIR_SORT=0)
   *) echo "unknown run: $NAME" >&2; exit 2 ;;
 esac
