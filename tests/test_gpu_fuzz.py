@@ -104,13 +104,9 @@ def test_zero_friction_coefficient_vs_oracle(gpu, orc):
     np.testing.assert_allclose(o["cost"], ref["cost"], rtol=1e-9, atol=1e-9)
 
 
-@pytest.mark.parametrize("seed", range(6))
-def test_fuzz_dense_vs_oracle(gpu, orc, seed):
-    """config E (the dense whole-body model: expm, Toeplitz condensing, 96-variable solve) with
-    the sampling time, torque bound and diagonal weights perturbed and odd batch sizes; U / cost
-    / status against the oracle, iteration counts with the workgroup crash caps"""
+def _draw_dense(seed):
+    """config E with the sampling time, torque bound and diagonal weights perturbed, odd batch"""
     import mpcqp
-    from mpcqp.engine import BatchEngine
     rng = np.random.default_rng(9100 + seed)
     p = mpcqp.model_params("E")
     nx = p["nx"]
@@ -122,7 +118,17 @@ def test_fuzz_dense_vs_oracle(gpu, orc, seed):
     p["P"] = np.diag(qd * rng.uniform(3.0, 20.0))
     p["R"] = np.asarray(p["R"], float) * rng.uniform(0.5, 2.0)
     B = int(rng.choice([1, 7, 33, 65, 127, 191]))
-    batch = mpcqp.make_batch(p, B, seed=9200 + seed)
+    return p, mpcqp.make_batch(p, B, seed=9200 + seed)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_fuzz_dense_vs_oracle(gpu, orc, seed):
+    """config E (the dense whole-body model: expm, Toeplitz condensing, 96-variable solve) with
+    the sampling time, torque bound and diagonal weights perturbed and odd batch sizes; U / cost
+    / status against the oracle, iteration counts with the workgroup crash caps"""
+    from mpcqp.engine import BatchEngine
+    p, batch = _draw_dense(seed)
+    B, lim = batch["x0"].shape[0], p["u_max"]
     eng = BatchEngine(p)
     crash = eng.crash
     d = eng.upload(batch)

@@ -3,7 +3,8 @@
 seeds than the committed test runs (config B / C / L; mass, inertia, friction, force bounds, Ts,
 weights, odd batch sizes, every gait), each against the oracle at the test's tolerances.
 Prints one line per failing draw and a summary.
-Usage:  python tools/fuzz_sweep.py [--first 24] [--count 200]"""
+--dense N adds N draws of the dense config E (test_fuzz_dense_vs_oracle's draws, seeds 6..).
+Usage:  python tools/fuzz_sweep.py [--first 24] [--count 200] [--dense 0]"""
 import argparse
 import os
 import sys
@@ -17,14 +18,24 @@ import numpy as np  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--first", type=int, default=24)
 ap.add_argument("--count", type=int, default=200)
+ap.add_argument("--dense", type=int, default=0)
 args = ap.parse_args()
 import oracle  # noqa: E402
 from mpcqp.engine import BatchEngine  # noqa: E402
-from test_gpu_fuzz import TOL_U, _draw  # noqa: E402
+from test_gpu_fuzz import TOL_U, _draw, _draw_dense  # noqa: E402
 
-bad = 0
-for seed in range(args.first, args.first + args.count):
-    p, batch, gait = _draw(seed)
+def draws():
+    for seed in range(args.first, args.first + args.count):
+        p, batch, gait = _draw(seed)
+        yield seed, p, batch, gait, False
+    for seed in range(6, 6 + args.dense):
+        p, batch = _draw_dense(seed)
+        yield seed, p, batch, "dense", True
+
+
+bad = n = 0
+for seed, p, batch, gait, dense in draws():
+    n += 1
     eng = BatchEngine(p)
     crash = eng.crash
     d = eng.upload(batch)
@@ -34,7 +45,8 @@ for seed in range(args.first, args.first + args.count):
     eng.close()
     q = dict(p)
     q["crash"] = tuple(crash)
-    ref = oracle.srbm_batch(q, batch["x0"], batch["xref"], batch["lin"], batch["contact"], nthreads=8)
+    ref = (oracle.dense_batch(q, batch["x0"], batch["xref"], batch["lin"]) if dense else
+           oracle.srbm_batch(q, batch["x0"], batch["xref"], batch["lin"], batch["contact"], nthreads=8))
     ok = ref["status"] == 0
     msgs = []
     if not np.array_equal(o["status"], ref["status"]):
@@ -52,4 +64,4 @@ for seed in range(args.first, args.first + args.count):
         bad += 1
         print(f"seed {seed} {p['config']} {gait} B={batch['x0'].shape[0]} mu={p['mu']:.3f} "
               f"fz_min={p['fz_min']:.2f}: " + "; ".join(msgs), flush=True)
-print(f"{args.count - bad} / {args.count} draws match the oracle")
+print(f"{n - bad} / {n} draws match the oracle")
