@@ -85,5 +85,6 @@ case "$NAME" in
   crash-gj2)   timeout -k 10 300 python3 tools/cmp_libs.py mpc-limx-control_amd/lib/libmpcqp.so mpc-limx-control_amd/lib/libmpcqp_gj2.so &&
                log rep 3 ab_b gj2 ;;                   # crash Gauss-Jordan, two pivots per round trip
   pair-sort)   log rep 3 ab_b nosort ;;                 # schedule-sorted pairing off (nosort: -DMPCQP_PAIR_SORT=0)
+  toep-pipe)   log rep 3 ab_e default toeppipe_e ;;     # E: software-pipelined Toeplitz tiles (NOILP=1 TU=fast_dense toeppipe_e:-DMPCQP_TOEP_PIPE=1)
   *) echo "unknown run: $NAME" >&2; exit 2 ;;
 esac
