@@ -143,7 +143,7 @@ __device__ __forceinline__ void wg_pick(const double *red, int o, double &v, int
 #define MPCQP_WG_CRASH_K 32
 #endif
 #ifndef MPCQP_WG_CRASH_P
-#define MPCQP_WG_CRASH_P 12
+#define MPCQP_WG_CRASH_P 8
 #endif
 constexpr int kWgCrashK = MPCQP_WG_CRASH_K, kWgCrashP = MPCQP_WG_CRASH_P;
 #ifndef MPCQP_WG_SRBM_CRASH
