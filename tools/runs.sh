@@ -86,5 +86,6 @@ case "$NAME" in
                log rep 3 ab_b gj2 ;;                   # crash Gauss-Jordan, two pivots per round trip
   pair-sort)   log rep 3 ab_b nosort ;;                 # schedule-sorted pairing off (nosort: -DMPCQP_PAIR_SORT=0)
   toep-pipe)   log rep 3 ab_e default toeppipe_e ;;     # E: software-pipelined Toeplitz tiles (NOILP=1 TU=fast_dense toeppipe_e:-DMPCQP_TOEP_PIPE=1)
+  wg-crash-k)  log rep 3 ab_e default kc24_e kc16_e ;;   # E: workgroup crash KC (NOILP=1 TU=fast_dense kc24_e:-DMPCQP_WG_CRASH_K=24 ...)
   *) echo "unknown run: $NAME" >&2; exit 2 ;;
 esac
