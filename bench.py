@@ -7,8 +7,8 @@ support) in `config.per_config` (N = 1 only).
 
 One step = one pass of the hot path over the rank's shard, inputs resident in HBM:
   k_mpc_pair (linearise + discretise + condense + Goldfarb-Idnani solve, fused, two QPs per
-  wavefront) -> k_mpc_wg (the overflow list's instances; empty for the alternating gait) whose
-  last workgroup writes the per-rank selection record [min key | winner's U]
+  wavefront) -> k_mpc_list (the overflow list's instances, one QP per wavefront; empty for the
+  alternating gait) whose last workgroup writes the per-rank selection record [min key | U]
   (mpcqp_batch_solve_select, the default `--select fused`: 0.376 vs 0.383 ms per step at
   65,536, 69 vs 76 us at 4,096; `--select separate` adds the k_select_min launch instead)
   -> [N>1] ONE RCCL all-gather of the records (8 + 480 B per rank) -> k_reduce_records.
@@ -236,9 +236,12 @@ def cpu_baseline(p, batch, budget_s=12.0):
                        f"{quota}), {dt:.1f} s; 1 thread: {n1} instances")
 
 
-def host_staged_rate(eng, batch, p, reps=5):
+def host_staged_rate(eng, batch, p, reps=5, locked=False):
     """QP/s through mpcqp_batch_solve_host: host arrays in, H2D + fused kernel + D2H, synchronous
-    (the PCIe-inclusive number; never `value`)."""
+    (the PCIe-inclusive number; never `value`).  locked: the caller's arrays are
+    page-locked once beforehand (mpcqp_host_register, as a controller allocating its buffers
+    once would), so the library DMAs straight from / into them in pipelined chunks; otherwise
+    pageable arrays through the context's pinned staging (a host memcpy each way)."""
     import ctypes as C
 
     from mpcqp._lib import lib
@@ -250,13 +253,22 @@ def host_staged_rate(eng, batch, p, reps=5):
     it = np.zeros(B, np.int32)
     ins = [np.ascontiguousarray(batch[k]) for k in ("x0", "xref", "lin", "contact")]
     ptr = lambda a: C.c_void_p(a.ctypes.data)
+    arrs = ins + [U, cost, st, it]
+    if locked:
+        for a in arrs:
+            assert lib().mpcqp_host_register(ptr(a), C.c_size_t(a.nbytes)) == 0
     call = lambda: lib().mpcqp_batch_solve_host(eng.ctx, B, *[ptr(a) for a in ins], ptr(U),
                                                  ptr(cost), ptr(st), ptr(it))
-    assert call() == 0
-    t = time.perf_counter()
-    for _ in range(reps):
-        call()
-    return B * reps / (time.perf_counter() - t)
+    try:
+        assert call() == 0
+        t = time.perf_counter()
+        for _ in range(reps):
+            call()
+        return B * reps / (time.perf_counter() - t)
+    finally:
+        if locked:
+            for a in arrs:
+                lib().mpcqp_host_unregister(ptr(a))
 
 
 def per_tick_latency(p, seed, ticks=1000, warmup=50, device=0):
@@ -654,7 +666,7 @@ def main():
             for _ in range(steps):
                 step()
             sync()
-            for w, name in ((2, eng.fused_kernel), (3, "k_mpc_wg")):
+            for w, name in ((2, eng.fused_kernel), (3, eng.overflow_kernel)):
                 ms, n = eng.kernel_ms_sum(w)
                 if n:
                     kern[name] = dict(ms=ms / n, launches=n)
@@ -695,7 +707,7 @@ def main():
                 for _ in range(steps):
                     step()
                 sync()
-                for w, name in ((2, eng.fused_kernel), (3, "k_mpc_wg")):
+                for w, name in ((2, eng.fused_kernel), (3, eng.overflow_kernel)):
                     ms, n = eng.kernel_ms_sum(w)
                     if n:
                         kern[name] = dict(ms=ms / n, launches=n)
@@ -864,7 +876,13 @@ def main():
         if weak:
             cfg["weak"] = weak
         if world == 1 and not args.no_host_path:
-            cfg["pcie_inclusive_qps"] = host_staged_rate(eng, local_batch, p)
+            cfg["pcie_inclusive_qps"] = host_staged_rate(eng, local_batch, p, locked=True)
+            cfg["pcie_inclusive_qps_pageable"] = host_staged_rate(eng, local_batch, p)
+            cfg["pcie_inclusive_note"] = (
+                "mpcqp_batch_solve_host, host arrays in / out, synchronous: pcie_inclusive_qps "
+                "with the caller's arrays page-locked once (mpcqp_host_register: DMA straight "
+                "from / into them, chunks pipelined over three streams), _pageable through the "
+                "context's pinned staging (a host memcpy each way)")
             cfg["gait_fused_qps"] = gait_fused_rate(eng, p, B, args.seed)
             cfg["per_tick_latency"] = per_tick_latency(p, args.seed, device=local)
         out["config"] = cfg

@@ -184,6 +184,10 @@ int mpcqp_ctx_fast_path(const mpcqp_ctx *ctx);
  * otherwise; 0 on the generic path): an instance with more goes to the overflow workgroup kernel
  * (bench.py counts the one-wave kernel's work over the instances it solved) */
 int mpcqp_ctx_one_wave_nf(const mpcqp_ctx *ctx);
+/* the overflow launch that follows the one-wave kernel on this context: 0 none (generic path,
+ * dense model, or no instance can exceed the one-wave kernel), 1 k_mpc_list (one QP per
+ * wavefront, a resident grid over the list: N = 10), 2 k_mpc_wg (one workgroup per QP) */
+int mpcqp_ctx_overflow_kernel(const mpcqp_ctx *ctx);
 /* the crash start of the context's kernels (a speculative primal-dual active-set start before the
  * dual loop): at most *kmax bounds per working set, *pmax working sets
  * before it falls back to the plain dual loop, for the one-wave kernel (the paired kernel) and
@@ -215,10 +219,25 @@ int mpcqp_batch_solve(mpcqp_ctx *ctx, int B, const double *x0, const double *xre
                       int *status, int *iters);
 /* Host-pointer convenience for controllers (one tick, B = 1 state x C candidates): copies the
  * host arrays (same layouts as above) into context-owned device buffers, runs
- * mpcqp_batch_solve and copies U/cost/status/iters back; synchronous. */
+ * mpcqp_batch_solve and copies U/cost/status/iters back; synchronous.
+ * Pageable arrays (and batches below 4,096) go through context-owned pinned staging: one host
+ * memcpy and one DMA each way (small batches replay a captured HIP graph).  When every array is
+ * page-locked (mpcqp_host_register / mpcqp_host_alloc) and B >= 4,096, the arrays are DMA'd
+ * straight from and into the caller's memory, no memcpy, in chunks of >= 8,192 instances
+ * pipelined over three streams (the copy-in of a chunk beside the solve of the previous one);
+ * results are identical either way (MPCQP_HOST_DIRECT=0 at context creation: always stage). */
 int mpcqp_batch_solve_host(mpcqp_ctx *ctx, int B, const double *x0, const double *xref,
                            const double *lin, const uint64_t *contact, double *U, double *cost,
                            int *status, int *iters);
+/* Page-locked host memory for the host-pointer entry points (src/QPSolver.cpp:93-96 hands the
+ * caller's own buffers to the solver; here the device reads them by DMA).  register / unregister
+ * wrap an existing allocation (the caller keeps it alive while registered: unregister before
+ * freeing it); alloc / free return new page-locked memory.  Registering is expensive (page
+ * pinning): do it once per buffer, not per tick. */
+int mpcqp_host_register(void *p, size_t bytes);
+int mpcqp_host_unregister(void *p);
+int mpcqp_host_alloc(size_t bytes, void **p);
+int mpcqp_host_free(void *p);
 
 /* key = (order-preserving bits of (float)cost << 31) | (index_base + i), min over the batch,
  * written to *key (device int64).  Instances with status != OK never win.  The caller
@@ -283,7 +302,16 @@ mpcqp_ctx *mpcqp_group_ctx(mpcqp_group *g, int i);
  * on the group's collective stream of that device, so this step's collective overlaps the next
  * step's solve.  best[i] is complete after mpcqp_group_sync, or, for work enqueued afterwards on
  * the member's context stream, after mpcqp_group_wait.  Records alternate between two buffers:
- * a step's solve waits (on device) for the all-gather two steps back, nothing else. */
+ * a step's solve waits (on device) for the all-gather two steps back, nothing else.
+ * Inputs: the solve runs on the member's own (non-blocking) context stream, which nothing orders
+ * after the caller's streams.  Inputs written by host copies must be complete (synchronised)
+ * before the call; inputs produced on a device stream need mpcqp_group_wait_stream first.
+ * Failure: arguments are checked before anything is enqueued (MPCQP_ERR_BAD_ARG, the group
+ * unchanged).  A failure after that -- part-way through the step, when peer ranks may already
+ * wait in its all-gather -- aborts the group's communicators (ncclCommAbort: the peers'
+ * collectives fail instead of hanging) and leaves the group failed: this and every later call
+ * but mpcqp_group_info / _failed / _destroy return MPCQP_ERR_DEVICE.  Destroy it on every rank
+ * and create a new group. */
 int mpcqp_group_solve_select(mpcqp_group *g, const int *B, const int64_t *base,
                              const double *const *x0, const double *const *xref,
                              const double *const *lin, const uint64_t *const *contact,
@@ -292,6 +320,13 @@ int mpcqp_group_solve_select(mpcqp_group *g, const int *B, const int64_t *base,
 /* make each member's context stream wait (on device) for its collective stream: results of the
  * steps issued so far are visible to work enqueued on the context streams afterwards */
 int mpcqp_group_wait(mpcqp_group *g);
+/* make local member i's context stream wait (on device) for the work enqueued so far on
+ * streams[i] (a hipStream_t of member i's device; NULL = its null stream): call it before
+ * mpcqp_group_solve_select when that stream produced the step's inputs (e.g. torch's current
+ * stream), instead of a host synchronisation */
+int mpcqp_group_wait_stream(mpcqp_group *g, void *const *streams);
+/* 1 once a step failed part-way (see mpcqp_group_solve_select), else 0 */
+int mpcqp_group_failed(const mpcqp_group *g);
 /* wait on the host for every member's streams */
 int mpcqp_group_sync(mpcqp_group *g);
 /* Host-pointer form for a single-process group (mpcqp_group_create; every rank local): the global

@@ -1,17 +1,38 @@
 // compat/MPCParam.h -- drop-in for the reference's include/MPCParam.h: the same public fields
-// (include/MPCParam.h:13-59, float timing fields kept float) and errorTest(), without the
-// limxsdk include it does not use.  The constructor is inline (the reference defines it in the
-// header non-inline, which breaks when two translation units include it).
+// (include/MPCParam.h:13-59, float timing fields kept float), the same include set, and
+// errorTest().  The constructor is inline (the reference defines it in the header non-inline,
+// which breaks when two translation units include it).
+//
+// errorTest (include/MPCParam.h:75-82) calls an unqualified abs() on a float difference at
+// global scope.  Which abs that is depends on the declarations visible there: with only the
+// <cmath> / <cstdlib> family it is C's int abs(int), so the difference is TRUNCATED to an
+// integer (any error below 1 rad passes the 0.1 rad test); once libstdc++'s <stdlib.h> or
+// <math.h> wrapper is visible (`using std::abs`: x86-64 Eigen pulls it in through the SSE
+// intrinsics headers -> <mm_malloc.h> -> <stdlib.h>) it is the float overload.  The body below
+// is written the reference's way, after the reference's includes, so it resolves to the same
+// abs as the reference does in the same translation unit.  MPCQP_ERRORTEST_ABS overrides it:
+//   0 (default) the reference's unqualified abs, as resolved here
+//   1           C's int abs on the truncated difference, whatever is included
+//   2           the float absolute value, whatever is included
 #ifndef MPCQP_COMPAT_MPC_PARAM_H
 #define MPCQP_COMPAT_MPC_PARAM_H
 
+#if __has_include("limxsdk/datatypes.h")
+#include "limxsdk/datatypes.h"
+#endif
 #include <cmath>
+#include <cstdlib>
+#include <iostream>
 #include <vector>
 
 #if __has_include(<Eigen/Dense>)
 #include <Eigen/Dense>
 #else
 #error "compat/MPCParam.h needs Eigen 3 (as the reference does)"
+#endif
+
+#ifndef MPCQP_ERRORTEST_ABS
+#define MPCQP_ERRORTEST_ABS 0
 #endif
 
 struct kinematicValues {
@@ -50,12 +71,30 @@ class MPCParam {
     Eigen::Vector3d static_foot_offset_right;
     Eigen::Vector3d static_foot_offset_left;
 
-    // include/MPCParam.h:75-82: true when all 6 joints are within givenErrorRate
+    // include/MPCParam.h:75-82: true when all 6 joints are within givenErrorRate (see the
+    // header comment for which abs the reference's expression means)
     bool errorTest(std::vector<float> targetPos, std::vector<float> nowPos) {
         bool ok = true;
-        for (int i = 0; i < 6; ++i)
+        for (int i = 0; i < 6; ++i) {
+#if MPCQP_ERRORTEST_ABS == 1
+            if (std::abs(static_cast<int>(targetPos[i] - nowPos[i])) >= givenErrorRate) ok = false;
+#elif MPCQP_ERRORTEST_ABS == 2
             if (std::fabs(targetPos[i] - nowPos[i]) >= givenErrorRate) ok = false;
+#else
+            if (abs(targetPos[i] - nowPos[i]) >= givenErrorRate) ok = false;
+#endif
+        }
         return ok;
+    }
+    // which abs errorTest applies in this translation unit: true = C's int abs (truncating)
+    static bool errorTestTruncates() {
+#if MPCQP_ERRORTEST_ABS == 1
+        return true;
+#elif MPCQP_ERRORTEST_ABS == 2
+        return false;
+#else
+        return abs(0.5f) == 0;
+#endif
     }
 };
 

@@ -18,6 +18,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -43,6 +44,7 @@ struct Member {
     hipEvent_t ev_gath[2] = {nullptr, nullptr};  // the all-gather of parity p has read rec[p]
     bool gath_pending[2] = {false, false};
     hipEvent_t ev_coll = nullptr;  // mpcqp_group_wait
+    hipEvent_t ev_in = nullptr;    // mpcqp_group_wait_stream: the caller's inputs are ready
     // host path: device staging [x0 | xref | lin | contact | U | cost | status | iters | best]
     // and its pinned mirror
     char *dbuf = nullptr;
@@ -60,7 +62,10 @@ struct mpcqp_group {
     mpcqp_model m{};
     int nranks = 0, first = 0, nV = 0, lin_w = 0;
     int par = 0;
-    bool whole = false;  // single process: every rank is a local member
+    bool whole = false;   // single process: every rank is a local member
+    bool failed = false;  // a step failed part-way: communicators aborted, every call refused
+    long step = 0;        // steps issued
+    long inject = -1;     // fault injection (tests): step MPCQP_GROUP_INJECT_FAIL fails part-way
     std::vector<Member> mem;
 };
 
@@ -82,7 +87,8 @@ int member_init(mpcqp_group *g, Member &mb) {
             hipEventCreateWithFlags(&mb.ev_gath[p], hipEventDisableTiming) != hipSuccess)
             return MPCQP_ERR_DEVICE;
     if (hipEventCreateWithFlags(&mb.ev_rec, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&mb.ev_coll, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&mb.ev_coll, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&mb.ev_in, hipEventDisableTiming) != hipSuccess)
         return MPCQP_ERR_DEVICE;
     return MPCQP_OK;
 }
@@ -101,11 +107,26 @@ void member_free(Member &mb) {
     }
     if (mb.ev_rec) hipEventDestroy(mb.ev_rec);
     if (mb.ev_coll) hipEventDestroy(mb.ev_coll);
+    if (mb.ev_in) hipEventDestroy(mb.ev_in);
     hipFree(mb.dbuf);
     if (mb.pin) hipHostFree(mb.pin);
     if (mb.ss) hipStreamDestroy(mb.ss);
     if (mb.cs) hipStreamDestroy(mb.cs);
     mb = Member();
+}
+
+// A step that fails after its first enqueue would leave peer ranks blocked in that step's
+// all-gather: abort every local communicator (peers' collectives then fail instead of hanging)
+// and refuse every later call.  The group must be destroyed on every rank.
+int group_fail(mpcqp_group *g) {
+    g->failed = true;
+    for (auto &mb : g->mem) {
+        if (!mb.comm) continue;
+        hipSetDevice(mb.device);
+        ncclCommAbort(mb.comm);
+        mb.comm = nullptr;
+    }
+    return MPCQP_ERR_DEVICE;
 }
 
 mpcqp_group *group_new(const mpcqp_model *m, int nranks) {
@@ -116,6 +137,7 @@ mpcqp_group *group_new(const mpcqp_model *m, int nranks) {
     g->nranks = nranks;
     g->nV = m->nu * m->N;
     g->lin_w = m->model == MPCQP_MODEL_DENSE ? m->nx * (m->nx + m->nu) : 8;
+    if (const char *e = getenv("MPCQP_GROUP_INJECT_FAIL")) g->inject = atol(e);
     return g;
 }
 
@@ -239,28 +261,34 @@ int mpcqp_group_solve_select(mpcqp_group *g, const int *B, const int64_t *base,
                              int *const *iters, int64_t *const *best) {
     if (!g || !B || !base || !x0 || !xref || !lin || !U || !cost || !status || !iters || !best)
         return MPCQP_ERR_BAD_ARG;
+    if (g->failed) return MPCQP_ERR_DEVICE;
     const int n = (int)g->mem.size();
     for (int i = 0; i < n; ++i)
-        if (B[i] < 0 || !best[i]) return MPCQP_ERR_BAD_ARG;
+        if (B[i] < 0 || !best[i] || !x0[i] || !xref[i] || !lin[i] || !U[i] || !cost[i] ||
+            !status[i] || !iters[i] ||
+            (g->m.model == MPCQP_MODEL_SRBM && (!contact || !contact[i])))
+            return MPCQP_ERR_BAD_ARG;
     const int p = g->par;
+    // from here on a failure is part-way through the step (group_fail)
     // solves (each on its member's solve stream), each followed by "record written"
     for (int i = 0; i < n; ++i) {
         Member &mb = g->mem[i];
-        if (hipSetDevice(mb.device) != hipSuccess) return MPCQP_ERR_DEVICE;
+        if (hipSetDevice(mb.device) != hipSuccess) return group_fail(g);
         // rec[p] is free once the all-gather two steps back has read it
         if (mb.gath_pending[p] && hipStreamWaitEvent(mb.ss, mb.ev_gath[p], 0) != hipSuccess)
-            return MPCQP_ERR_DEVICE;
+            return group_fail(g);
         int rc = mpcqp_batch_solve_select(mb.ctx, B[i], x0[i], xref[i], lin[i],
                                           contact ? contact[i] : nullptr, U[i], cost[i],
                                           status[i], iters[i], base[i], mb.rec[p]);
-        if (rc) return rc;
+        if (rc) return group_fail(g);
         if (hipEventRecord(mb.ev_rec, mb.ss) != hipSuccess ||
             hipStreamWaitEvent(mb.cs, mb.ev_rec, 0) != hipSuccess)
-            return MPCQP_ERR_DEVICE;
+            return group_fail(g);
     }
+    if (g->step++ == g->inject) return group_fail(g);  // (tests: a failure after the solves)
     // ONE all-gather of the records over all ranks (grouped over this process's members)
     const size_t cnt = 1 + (size_t)g->nV;
-    if (n > 1 && ncclGroupStart() != ncclSuccess) return MPCQP_ERR_DEVICE;
+    if (n > 1 && ncclGroupStart() != ncclSuccess) return group_fail(g);
     int rc = MPCQP_OK;
     for (int i = 0; i < n && !rc; ++i) {
         Member &mb = g->mem[i];
@@ -268,21 +296,37 @@ int mpcqp_group_solve_select(mpcqp_group *g, const int *B, const int64_t *base,
         rc = nccl_rc(ncclAllGather(mb.rec[p], mb.gath[p], cnt, ncclInt64, mb.comm, mb.cs));
     }
     if (n > 1 && ncclGroupEnd() != ncclSuccess) rc = MPCQP_ERR_DEVICE;
-    if (rc) return rc;
+    if (rc) return group_fail(g);
     for (int i = 0; i < n; ++i) {
         Member &mb = g->mem[i];
         hipSetDevice(mb.device);
-        if (hipEventRecord(mb.ev_gath[p], mb.cs) != hipSuccess) return MPCQP_ERR_DEVICE;
+        if (hipEventRecord(mb.ev_gath[p], mb.cs) != hipSuccess) return group_fail(g);
         mb.gath_pending[p] = true;
         rc = mpcqp_reduce_records_on(mb.ctx, mb.cs, g->nranks, mb.gath[p], best[i]);
-        if (rc) return rc;
+        if (rc) return group_fail(g);
     }
     g->par ^= 1;
     return MPCQP_OK;
 }
 
+int mpcqp_group_wait_stream(mpcqp_group *g, void *const *streams) {
+    if (!g || !streams) return MPCQP_ERR_BAD_ARG;
+    if (g->failed) return MPCQP_ERR_DEVICE;
+    for (size_t i = 0; i < g->mem.size(); ++i) {
+        Member &mb = g->mem[i];
+        if (hipSetDevice(mb.device) != hipSuccess ||
+            hipEventRecord(mb.ev_in, (hipStream_t)streams[i]) != hipSuccess ||
+            hipStreamWaitEvent(mb.ss, mb.ev_in, 0) != hipSuccess)
+            return MPCQP_ERR_DEVICE;
+    }
+    return MPCQP_OK;
+}
+
+int mpcqp_group_failed(const mpcqp_group *g) { return g && g->failed ? 1 : 0; }
+
 int mpcqp_group_wait(mpcqp_group *g) {
     if (!g) return MPCQP_ERR_BAD_ARG;
+    if (g->failed) return MPCQP_ERR_DEVICE;
     for (auto &mb : g->mem) {
         if (hipSetDevice(mb.device) != hipSuccess ||
             hipEventRecord(mb.ev_coll, mb.cs) != hipSuccess ||
@@ -294,7 +338,7 @@ int mpcqp_group_wait(mpcqp_group *g) {
 
 int mpcqp_group_sync(mpcqp_group *g) {
     if (!g) return MPCQP_ERR_BAD_ARG;
-    int rc = MPCQP_OK;
+    int rc = g->failed ? MPCQP_ERR_DEVICE : MPCQP_OK;
     for (auto &mb : g->mem) {
         hipSetDevice(mb.device);
         if (hipStreamSynchronize(mb.ss) != hipSuccess) rc = MPCQP_ERR_DEVICE;
@@ -312,6 +356,7 @@ int mpcqp_group_solve_select_host(mpcqp_group *g, int S, int C, const double *x0
         return MPCQP_ERR_BAD_ARG;
     if (g->m.model == MPCQP_MODEL_SRBM && !contact) return MPCQP_ERR_BAD_ARG;
     if (!g->whole) return MPCQP_ERR_BAD_ARG;  // every rank's shard must be local
+    if (g->failed) return MPCQP_ERR_DEVICE;
     if ((long long)S * C > 0x7fffffffll) return MPCQP_ERR_BAD_DIMS;
     const int n = (int)g->mem.size();
     const size_t nx = g->m.nx, N = g->m.N, nV = g->nV, lw = g->lin_w;

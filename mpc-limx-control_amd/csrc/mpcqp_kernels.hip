@@ -448,6 +448,10 @@ bool pick_fast(int model, int nx, int nu, int N, bool fric, int nfmax, FastKerne
     // working sets (0: the plain dual loop from the unconstrained minimum; A/B runs and tests)
     if (k.pair && k.crash_k > 0)
         if (const char *e = getenv("MPCQP_CRASH_P")) k.crash_p = std::max(0, atoi(e));
+    // (diagnostic MPCQP_PAIR_LDS_PAD=bytes: extra LDS per paired-kernel wave, i.e. fewer resident
+    //  waves per CU -- the kernel's occupancy sensitivity, tools/ab_env.py; never in a measured line)
+    if (k.pair)
+        if (const char *e = getenv("MPCQP_PAIR_LDS_PAD")) k.pair_lds += (size_t)std::max(0, atoi(e));
     if (found) {
         k.prim_nf = k.pair ? kPairCap : k.nf;
         if (nfmax > k.prim_nf) add_fast_wg(model, N, fric, k);
@@ -562,6 +566,12 @@ struct mpcqp_ctx {
     size_t pin_cap = 0;
     hipStream_t hstream = nullptr;
     hipEvent_t hev = nullptr;
+    // the direct host path (the caller's page-locked arrays): copy-in / copy-out streams and the
+    // per-chunk "inputs landed" / "solved" events of the pipeline (created on first use)
+    hipStream_t hs_in = nullptr, hs_out = nullptr;
+    hipEvent_t hev_in[8] = {}, hev_k[8] = {};
+    bool hd_ok = false;
+    bool hd_off = false;  // MPCQP_HOST_DIRECT=0: always stage (A/B of the direct path)
     int hg_B = 0;
     unsigned long long buf_gen = 0, hg_gen = 0;
     hipGraphExec_t hg_exec[3] = {nullptr, nullptr, nullptr};
@@ -917,6 +927,7 @@ int mpcqp_ctx_create(const mpcqp_model *m, int device, mpcqp_ctx **out) {
     if (!c) return MPCQP_ERR_DEVICE;
     c->m = *m;
     c->device = device;
+    if (const char *e = getenv("MPCQP_HOST_DIRECT")) c->hd_off = atoi(e) == 0;
     inv3(m->Ib, c->Ibinv);
     const int nx = m->nx, nu = m->nu;
     double qd[MPCQP_MAX_NX], pd[MPCQP_MAX_NX];
@@ -986,6 +997,11 @@ int mpcqp_ctx_fast_path(const mpcqp_ctx *c) {
     return c->fk.pair ? 2 : 1;
 }
 
+int mpcqp_ctx_overflow_kernel(const mpcqp_ctx *c) {
+    if (!c || !c->fast || !c->fk.wg) return 0;
+    return c->fk.wg_threads == 64 ? 1 : 2;
+}
+
 int mpcqp_ctx_one_wave_nf(const mpcqp_ctx *c) {
     if (!c || !c->fast || c->fk.dense) return 0;
     return c->fk.prim_nf;
@@ -1007,8 +1023,9 @@ int mpcqp_count_solver_flops(mpcqp_ctx *c, int on) {
     if (!c) return MPCQP_ERR_BAD_ARG;
     if (on && !c->dflops) {
         hipSetDevice(c->device);
+        // (cleared on the context's stream: a later launch on it is ordered after the clear)
         if (hipMalloc(&c->dflops, sizeof(double) * kFlopsWords) != hipSuccess ||
-            hipMemset(c->dflops, 0, sizeof(double) * kFlopsWords) != hipSuccess) {
+            hipMemsetAsync(c->dflops, 0, sizeof(double) * kFlopsWords, c->stream) != hipSuccess) {
             hipFree(c->dflops);
             c->dflops = nullptr;
             return MPCQP_ERR_DEVICE;
@@ -1023,9 +1040,11 @@ double mpcqp_solver_flops(mpcqp_ctx *c, int *launches) {
     if (!c || !c->dflops) return -1.0;
     double h[kFlopsWords], v = 0.0;
     hipSetDevice(c->device);
-    if (hipStreamSynchronize(c->stream) != hipSuccess ||
-        hipMemcpy(h, c->dflops, sizeof h, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemset(c->dflops, 0, sizeof h) != hipSuccess)
+    // read and cleared on the context's stream (it may be non-blocking: a null-stream clear
+    // would not be ordered before the next launch's atomics)
+    if (hipMemcpyAsync(h, c->dflops, sizeof h, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipMemsetAsync(c->dflops, 0, sizeof h, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
         return -1.0;
     for (int i = 0; i < kFlopsSlots; ++i) v += h[i * kFlopsStride];
     if (launches) *launches = c->flops_launches;
@@ -1079,6 +1098,12 @@ int mpcqp_ctx_destroy(mpcqp_ctx *c) {
     if (c->pin) hipHostFree(c->pin);
     if (c->hev) hipEventDestroy(c->hev);
     if (c->hstream) hipStreamDestroy(c->hstream);
+    for (int i = 0; i < 8; ++i) {
+        if (c->hev_in[i]) hipEventDestroy(c->hev_in[i]);
+        if (c->hev_k[i]) hipEventDestroy(c->hev_k[i]);
+    }
+    if (c->hs_in) hipStreamDestroy(c->hs_in);
+    if (c->hs_out) hipStreamDestroy(c->hs_out);
     hipFree(c->rbuf);
     hipFree(c->fkbuf);
     hipFree(c->dwarm);
@@ -1669,6 +1694,120 @@ static void host_graphs_drop(mpcqp_ctx *c) {
     c->hg_B = 0;
 }
 
+// ---- page-locked host memory (the caller's own buffers handed to the solver, as
+// src/QPSolver.cpp:93-96 hands its Eigen storage to qpOASES): registered or allocated here, a host
+// array is DMA'd straight to and from the device by the host-pointer entry points
+int mpcqp_host_register(void *p, size_t bytes) {
+    if (!p || !bytes) return MPCQP_ERR_BAD_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MPCQP_ERR_NO_DEVICE;
+    return hip_status(hipHostRegister(p, bytes, hipHostRegisterDefault));
+}
+
+int mpcqp_host_unregister(void *p) {
+    if (!p) return MPCQP_ERR_BAD_ARG;
+    return hip_status(hipHostUnregister(p));
+}
+
+int mpcqp_host_alloc(size_t bytes, void **p) {
+    if (!p || !bytes) return MPCQP_ERR_BAD_ARG;
+    *p = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MPCQP_ERR_NO_DEVICE;
+    return hip_status(hipHostMalloc(p, bytes, hipHostMallocDefault));
+}
+
+int mpcqp_host_free(void *p) {
+    if (!p) return MPCQP_ERR_BAD_ARG;
+    return hip_status(hipHostFree(p));
+}
+
+// is [p, p + bytes) page-locked host memory the device can DMA (hipHostRegister / hipHostMalloc)?
+static bool host_locked(const void *p, size_t bytes) {
+    if (!p || !bytes) return false;
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    if (at.type != hipMemoryTypeHost) return false;
+    // the whole range must belong to one locked allocation: check its last byte as well
+    hipPointerAttribute_t at2;
+    if (hipPointerGetAttributes(&at2, (const char *)p + bytes - 1) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at2.type == hipMemoryTypeHost;
+}
+
+// batches below this go through the pinned staging and the captured graphs (the per-tick path)
+constexpr int kHostDirectMin = 4096;
+
+// The direct host path: inputs DMA'd from the caller's page-locked arrays into device staging and
+// outputs DMA'd back into the caller's arrays, no host memcpy.  The batch goes in chunks
+// (multiples of 16 instances: the paired kernel's candidate groups stay whole, so every instance
+// is solved exactly as in one launch), pipelined over three streams: the copy-in of chunk i + 1
+// and the copy-out of chunk i - 1 run beside the solve of chunk i.
+static int host_direct(mpcqp_ctx *c, int B, const double *x0, const double *xref,
+                       const double *lin, const uint64_t *contact, double *U, double *cost,
+                       int *status, int *iters, bool ovf, size_t out_off) {
+    if (!c->hd_ok) {
+        if (hipStreamCreateWithFlags(&c->hs_in, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&c->hs_out, hipStreamNonBlocking) != hipSuccess)
+            return MPCQP_ERR_DEVICE;
+        for (int i = 0; i < 8; ++i)
+            if (hipEventCreateWithFlags(&c->hev_in[i], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&c->hev_k[i], hipEventDisableTiming) != hipSuccess)
+                return MPCQP_ERR_DEVICE;
+        c->hd_ok = true;
+    }
+    const size_t nx = c->m.nx, N = c->m.N, nV = (size_t)c->m.nu * c->m.N;
+    const size_t lin_w = c->m.model == MPCQP_MODEL_DENSE ? nx * (nx + c->m.nu) : 8;
+    char *d = (char *)c->hbuf;
+    double *d_x0 = (double *)d, *d_xr = d_x0 + nx * B, *d_lin = d_xr + nx * (N + 1) * B;
+    uint64_t *d_ct = (uint64_t *)(d_lin + lin_w * B);
+    double *d_U = (double *)(d + out_off), *d_cost = d_U + nV * B;
+    int *d_st = (int *)(d_cost + B), *d_it = d_st + B;
+    // four chunks of >= 8,192 instances (at most 8), multiples of 16
+    int chunk = std::max(8192, (B / 4 + 15) & ~15);
+    if ((B + chunk - 1) / chunk > 8) chunk = ((B + 7) / 8 + 15) & ~15;
+    const int nch = (B + chunk - 1) / chunk;
+    // the copy-in waits for the context's earlier work (hev was recorded on its stream)
+    if (hipStreamWaitEvent(c->hs_in, c->hev, 0) != hipSuccess) return MPCQP_ERR_DEVICE;
+    const hipMemcpyKind h2d = hipMemcpyHostToDevice, d2h = hipMemcpyDeviceToHost;
+    for (int i = 0; i < nch; ++i) {
+        const size_t i0 = (size_t)i * chunk, n = std::min((size_t)chunk, (size_t)B - i0);
+        if (hipMemcpyAsync(d_x0 + i0 * nx, x0 + i0 * nx, 8 * nx * n, h2d, c->hs_in) != hipSuccess ||
+            hipMemcpyAsync(d_xr + i0 * nx * (N + 1), xref + i0 * nx * (N + 1), 8 * nx * (N + 1) * n,
+                           h2d, c->hs_in) != hipSuccess ||
+            hipMemcpyAsync(d_lin + i0 * lin_w, lin + i0 * lin_w, 8 * lin_w * n, h2d, c->hs_in) != hipSuccess ||
+            (contact && hipMemcpyAsync(d_ct + i0, contact + i0, 8 * n, h2d, c->hs_in) != hipSuccess) ||
+            hipEventRecord(c->hev_in[i], c->hs_in) != hipSuccess ||
+            hipStreamWaitEvent(c->hstream, c->hev_in[i], 0) != hipSuccess)
+            return MPCQP_ERR_DEVICE;
+        hipStream_t keep = c->stream;
+        const bool timing = c->timing;
+        c->stream = c->hstream;
+        c->timing = false;  // (the host path does not feed the timing slots)
+        const int rc = batch_solve(c, (int)n, d_x0 + i0 * nx, d_xr + i0 * nx * (N + 1),
+                                   d_lin + i0 * lin_w, contact ? d_ct + i0 : nullptr,
+                                   d_U + i0 * nV, d_cost + i0, d_st + i0, d_it + i0, ovf);
+        c->stream = keep;
+        c->timing = timing;
+        if (rc) return rc;
+        if (hipEventRecord(c->hev_k[i], c->hstream) != hipSuccess ||
+            hipStreamWaitEvent(c->hs_out, c->hev_k[i], 0) != hipSuccess ||
+            hipMemcpyAsync(U + i0 * nV, d_U + i0 * nV, 8 * nV * n, d2h, c->hs_out) != hipSuccess ||
+            hipMemcpyAsync(cost + i0, d_cost + i0, 8 * n, d2h, c->hs_out) != hipSuccess ||
+            hipMemcpyAsync(status + i0, d_st + i0, 4 * n, d2h, c->hs_out) != hipSuccess ||
+            hipMemcpyAsync(iters + i0, d_it + i0, 4 * n, d2h, c->hs_out) != hipSuccess)
+            return MPCQP_ERR_DEVICE;
+    }
+    if (hipStreamSynchronize(c->hs_out) != hipSuccess || hipStreamSynchronize(c->hstream) != hipSuccess)
+        return MPCQP_ERR_DEVICE;
+    return MPCQP_OK;
+}
+
 int mpcqp_batch_solve_host(mpcqp_ctx *c, int B, const double *x0, const double *xref,
                            const double *lin, const uint64_t *contact, double *U, double *cost,
                            int *status, int *iters) {
@@ -1689,6 +1828,23 @@ int mpcqp_batch_solve_host(mpcqp_ctx *c, int B, const double *x0, const double *
     const size_t out_bytes = b_u + b_c + 2 * b_i, total = out_off + out_bytes;
     if (ensure_bytes(c, &c->hbuf, &c->hbuf_cap, std::max(total, host_stage_bytes(c, B))))
         return MPCQP_ERR_DEVICE;
+    if (!c->hstream) {
+        if (hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&c->hev, hipEventDisableTiming) != hipSuccess)
+            return MPCQP_ERR_DEVICE;
+    }
+    const bool ovf = host_may_overflow(c, B, contact);
+    if (ovf && ensure_list(c, B)) return MPCQP_ERR_DEVICE;  // (allocates outside any capture)
+    // the caller's arrays page-locked (mpcqp_host_register / mpcqp_host_alloc) and a large batch:
+    // one DMA each way straight from / into them, pipelined in chunks
+    if (B >= kHostDirectMin && !c->hd_off && host_locked(x0, b_x0) && host_locked(xref, b_xr) &&
+        host_locked(lin, b_lin) && (!contact || host_locked(contact, b_ct)) &&
+        host_locked(U, b_u) && host_locked(cost, b_c) && host_locked(status, b_i) &&
+        host_locked(iters, b_i)) {
+        if (hipEventRecord(c->hev, c->stream) != hipSuccess) return MPCQP_ERR_DEVICE;
+        return host_direct(c, B, x0, xref, lin, contact, U, cost, status, iters, ovf, out_off);
+    }
+    // otherwise: one memcpy into the context's pinned staging and one DMA each way
     if (c->pin_cap < total) {
         if (c->pin) hipHostFree(c->pin);
         c->pin = nullptr;
@@ -1697,13 +1853,6 @@ int mpcqp_batch_solve_host(mpcqp_ctx *c, int B, const double *x0, const double *
         if (hipHostMalloc(&c->pin, total, hipHostMallocDefault) != hipSuccess) return MPCQP_ERR_DEVICE;
         c->pin_cap = total;
     }
-    if (!c->hstream) {
-        if (hipStreamCreateWithFlags(&c->hstream, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&c->hev, hipEventDisableTiming) != hipSuccess)
-            return MPCQP_ERR_DEVICE;
-    }
-    const bool ovf = host_may_overflow(c, B, contact);
-    if (ovf && ensure_list(c, B)) return MPCQP_ERR_DEVICE;  // (allocates outside any capture)
     // (after every allocation this call may make: a graph is captured against the buffers as
     // they are now)
     if (c->hg_gen != c->buf_gen) {

@@ -24,7 +24,7 @@ EXPORTS = [
     "mpcqp_discretize", "mpcqp_discretize_quadrature", "mpcqp_build_qp", "mpcqp_solve_dense", "mpcqp_plant_step",
     "mpcqp_ctx_create", "mpcqp_ctx_destroy", "mpcqp_set_stream", "mpcqp_sync",
     "mpcqp_batch_condense", "mpcqp_batch_solve_qp", "mpcqp_batch_solve",
-    "mpcqp_ctx_fast_path", "mpcqp_ctx_one_wave_nf", "mpcqp_ctx_crash_params", "mpcqp_batch_discretize", "mpcqp_batch_condense_solve",
+    "mpcqp_ctx_fast_path", "mpcqp_ctx_one_wave_nf", "mpcqp_ctx_overflow_kernel", "mpcqp_ctx_crash_params", "mpcqp_batch_discretize", "mpcqp_batch_condense_solve",
     "mpcqp_debug_phase_cycles", "mpcqp_batch_solve_host",
     "mpcqp_count_solver_flops", "mpcqp_solver_flops",
     "mpcqp_batch_select_min", "mpcqp_batch_select_record", "mpcqp_reduce_records",
@@ -36,6 +36,8 @@ EXPORTS = [
     "mpcqp_shard", "mpcqp_group_create", "mpcqp_group_unique_id", "mpcqp_group_create_rank",
     "mpcqp_group_destroy", "mpcqp_group_info", "mpcqp_group_ctx", "mpcqp_group_solve_select",
     "mpcqp_group_wait", "mpcqp_group_sync", "mpcqp_group_solve_select_host",
+    "mpcqp_group_wait_stream", "mpcqp_group_failed",
+    "mpcqp_host_register", "mpcqp_host_unregister", "mpcqp_host_alloc", "mpcqp_host_free",
     "mpcqp_status_string", "mpcqp_device_count", "mpcqp_build_id",
 ]
 
@@ -83,7 +85,8 @@ def lib():
     L.mpcqp_batch_solve_qp.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp]
     L.mpcqp_batch_solve.argtypes = [vp, i, vp, vp, vp, vp, vp, vp, vp, vp]
     L.mpcqp_ctx_fast_path.argtypes = [vp]
-    for name, at in (("mpcqp_ctx_one_wave_nf", [vp]), ("mpcqp_ctx_crash_params", [vp] + [vp] * 4)):
+    for name, at in (("mpcqp_ctx_one_wave_nf", [vp]), ("mpcqp_ctx_crash_params", [vp] + [vp] * 4),
+                     ("mpcqp_ctx_overflow_kernel", [vp])):
         if hasattr(L, name):  # absent from A/B builds of older sources
             getattr(L, name).argtypes = at
     L.mpcqp_debug_phase_cycles.argtypes = [vp, vp, i]
@@ -126,6 +129,13 @@ def lib():
         L.mpcqp_group_wait.argtypes = [vp]
         L.mpcqp_group_sync.argtypes = [vp]
         L.mpcqp_group_solve_select_host.argtypes = [vp, i, i] + [vp] * 9
+        L.mpcqp_group_wait_stream.argtypes = [vp, vp]
+        L.mpcqp_group_failed.argtypes = [vp]
+    if hasattr(L, "mpcqp_host_register"):  # absent from A/B builds of older sources
+        L.mpcqp_host_register.argtypes = [vp, C.c_size_t]
+        L.mpcqp_host_unregister.argtypes = [vp]
+        L.mpcqp_host_alloc.argtypes = [C.c_size_t, vp]
+        L.mpcqp_host_free.argtypes = [vp]
     L.mpcqp_status_string.argtypes = [i]
     L.mpcqp_status_string.restype = C.c_char_p
     L.mpcqp_build_id.argtypes = []

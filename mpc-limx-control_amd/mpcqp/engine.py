@@ -134,6 +134,15 @@ class BatchEngine:
         return {3: "k_dense_wg", 2: "k_mpc_pair", 1: "k_mpc"}.get(
             lib().mpcqp_ctx_fast_path(self.ctx), "k_condense+k_solve")
 
+    @property
+    def overflow_kernel(self) -> str:
+        """the overflow launch after the one-wave kernel (slot 3 of the library's timing):
+        k_mpc_list (one QP per wavefront), k_mpc_wg (one workgroup per QP) or none"""
+        L = lib()
+        if not hasattr(L, "mpcqp_ctx_overflow_kernel"):  # A/B builds of older sources
+            return "k_mpc_wg"
+        return {1: "k_mpc_list", 2: "k_mpc_wg"}.get(L.mpcqp_ctx_overflow_kernel(self.ctx), "none")
+
     def discretize(self, d, AB=None):
         """stage 1: linearise + exp(M Ts) -> [Ad | Bd] per instance"""
         t = self.torch

@@ -83,11 +83,19 @@ class Group:
         except Exception:
             pass
 
-    def solve_select(self, shards, best):
+    def solve_select(self, shards, best, after_current_stream=True):
         """shards: one dict per local member (torch tensors on its device: x0, xref, lin,
         contact, U, cost, status, iters, and "base": the global index of its first instance);
-        best: one int64 [1 + nV] tensor per member.  Asynchronous (group_sync / group_wait)."""
+        best: one int64 [1 + nV] tensor per member.  Asynchronous (group_sync / group_wait).
+        The group's solve streams first wait (on device) for torch's current stream of each
+        member's device, which produced the shards (mpcqp_group_wait_stream), unless
+        after_current_stream is False."""
         n = self.local
+        if after_current_stream:
+            import torch
+            streams = (C.c_void_p * n)(*[torch.cuda.current_stream(s["x0"].device).cuda_stream
+                                         for s in shards])
+            check("mpcqp_group_wait_stream", lib().mpcqp_group_wait_stream(self.g, streams))
         Bs = (C.c_int * n)(*[int(s["x0"].shape[0]) for s in shards])
         bases = (C.c_int64 * n)(*[int(s["base"]) for s in shards])
         col = lambda k: _ptrs([s[k] for s in shards])
@@ -95,6 +103,10 @@ class Group:
               lib().mpcqp_group_solve_select(self.g, Bs, bases, col("x0"), col("xref"), col("lin"),
                                              col("contact"), col("U"), col("cost"), col("status"),
                                              col("iters"), _ptrs(best)))
+
+    @property
+    def failed(self) -> bool:
+        return bool(lib().mpcqp_group_failed(self.g))
 
     def wait(self):
         check("mpcqp_group_wait", lib().mpcqp_group_wait(self.g))

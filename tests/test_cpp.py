@@ -66,6 +66,31 @@ def test_compat_headers_need_eigen(tmp_path):
         assert r.returncode != 0 and "needs Eigen" in r.stderr, (h, r.stderr)
 
 
+@pytest.mark.parametrize("flags,trunc", [
+    ((), 1),                                                   # the <cmath> family only: int abs
+    (("-include", "emmintrin.h"), 0),                          # x86-64 Eigen's SSE headers: float
+    (("-include", "emmintrin.h", "-DMPCQP_ERRORTEST_ABS=1"), 1),  # forced int abs
+    (("-DMPCQP_ERRORTEST_ABS=2",), 0),                         # forced float abs
+])
+def test_compat_mpcparam_errortest(tmp_path, flags, trunc):
+    """MPCParam::errorTest (include/MPCParam.h:75-82) reproduces the abs() the reference's
+    unqualified call resolves to in the same translation unit -- C's int abs on the truncated
+    difference unless libstdc++'s <stdlib.h> / <math.h> wrapper is visible -- and leaves
+    src/mpc_control_fake_state.cpp:57-89's start-up loop at the restatement's iteration."""
+    exe = str(tmp_path / "errortest")
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-Werror", *flags,
+           f"-DEXPECT_TRUNC={trunc}", "-I", SHIM, "-I", COMPAT,
+           os.path.join(ROOT, "tests", "cpp", "errortest.cpp"), "-o", exe]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 0 and "errortest OK" in r.stdout, r.stdout + r.stderr
+    ex = int(r.stdout.split("exit=")[1].split()[0])
+    # every joint starts 0.5-1.75 rad off: the truncating test passes once all are under 1 rad,
+    # the float test only once all are under 0.1 rad
+    assert (ex < 1000) if trunc else (ex > 1800), r.stdout
+
+
 @pytest.mark.gpu
 def test_cpp_qp_test_loop_matches_golden(gpu, golden, exes):
     g = golden("a0_harness.npz")

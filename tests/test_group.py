@@ -4,7 +4,10 @@ CPU: the shard arithmetic every multi-GPU path shares (mpcqp_shard, host code in
 against a restatement and the cover / balance properties; the group entry points refuse bad
 arguments without touching a device.  GPU: a one-rank group (mpcqp_group_create_rank with the
 library's own RCCL communicator, and mpcqp_group_create over device 0) gives, step after step,
-the record and per-instance outputs of one context's mpcqp_batch_solve_select bit for bit."""
+the record and per-instance outputs of one context's mpcqp_batch_solve_select bit for bit; a
+group over EVERY visible device (skipped on a one-GPU box) gives the whole batch's record on
+every member; the solve waits for the stream that produced its inputs; a step that fails
+part-way leaves the group failed (communicators aborted, later calls refused)."""
 import ctypes as C
 
 import numpy as np
@@ -108,3 +111,132 @@ def test_group_host_path_matches_solve_select(gpu):
         assert np.array_equal(out["iters"], dr["iters"].cpu().numpy())
     grp.close()
     ref.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gait", ["alternating", "mixed"])
+def test_group_all_devices_matches_whole_batch(gpu, gait):
+    """mpcqp_group_create over every visible device (ncclCommInitAll, the grouped all-gather of
+    the local members, the cross-rank reduction, both record buffers over three steps): each
+    member's best record equals one context's mpcqp_batch_solve_select over the WHOLE batch, bit
+    for bit, and the per-instance outputs of each shard equal that context's.  Needs >= 2
+    devices (src/mpc_control_fake_state.cpp:108-149 at batch scale)."""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    from mpcqp.group import Group, shard
+    torch = gpu
+    ndev = torch.cuda.device_count()
+    if ndev < 2:
+        pytest.skip("one visible device: the multi-device group needs >= 2")
+    p = mpcqp.model_params("B")
+    Cn = 16
+    S = 37 * ndev + 3  # uneven shards
+    batch = mpcqp.make_batch(p, S * Cn, seed=8080, gait=gait)
+    ref = BatchEngine(p, device=0)
+    dr = ref.upload(batch)
+    rec = torch.zeros(1 + ref.nV, dtype=torch.int64, device="cuda:0")
+    ref.solve_select(dr, rec)
+    ref.sync()
+    grp = Group(p, devices=list(range(ndev)))
+    assert (grp.local, grp.nranks, grp.first_rank) == (ndev, ndev, 0)
+    engs, shards = [], []
+    for r in range(ndev):
+        f, n = shard(S, ndev, r)
+        sub = {k: v[f * Cn:(f + n) * Cn] for k, v in batch.items()}
+        e = BatchEngine.wrap(p, grp.ctx(r), r)
+        d = e.upload(sub)
+        engs.append(e)
+        shards.append(dict(d, base=f * Cn))
+    steps = [[torch.full((1 + ref.nV,), -5, dtype=torch.int64, device=f"cuda:{r}")
+              for r in range(ndev)] for _ in range(3)]
+    for best in steps:
+        grp.solve_select(shards, best)
+    grp.sync()
+    want = rec.cpu()
+    for best in steps:
+        for b_ in best:
+            assert torch.equal(b_.cpu(), want)
+    for r in range(ndev):
+        f, n = shard(S, ndev, r)
+        for k in ("U", "cost", "status", "iters"):
+            assert torch.equal(shards[r][k].cpu(), dr[k][f * Cn:(f + n) * Cn].cpu()), (r, k)
+    for e in engs:
+        e.close()
+    grp.close()
+    ref.close()
+
+
+@pytest.mark.gpu
+def test_group_solve_waits_for_the_input_stream(gpu):
+    """inputs written on a torch stream that is still busy (a spin kernel ahead of the copies):
+    the group's own solve stream waits for it (mpcqp_group_wait_stream, Group.solve_select's
+    default) with no host synchronisation, and the step's results are the inputs' results"""
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    from mpcqp.group import Group, unique_id
+    torch = gpu
+    p = mpcqp.model_params("B")
+    B = 16 * 64
+    batch = mpcqp.make_batch(p, B, seed=91)
+    ref = BatchEngine(p)
+    dr = ref.upload(batch)
+    rec = torch.zeros(1 + ref.nV, dtype=torch.int64, device="cuda:0")
+    ref.solve_select(dr, rec)
+    ref.sync()
+    grp = Group(p, rank=(0, 1, 0, unique_id()))
+    eng = BatchEngine.wrap(p, grp.ctx(0), 0)
+    d = eng.upload(mpcqp.make_batch(p, B, seed=92))  # other inputs, overwritten below
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(50_000_000)  # ~20 ms of spinning ahead of the input copies
+        for k in ("x0", "xref", "lin", "contact"):
+            d[k].copy_(dr[k])
+        best = torch.full((1 + ref.nV,), -5, dtype=torch.int64, device="cuda:0")
+        grp.solve_select([dict(d, base=0)], [best])
+    grp.sync()
+    side.synchronize()
+    assert torch.equal(best, rec)
+    for k in ("U", "cost", "status", "iters"):
+        assert torch.equal(d[k], dr[k]), k
+    eng.close()
+    grp.close()
+    ref.close()
+
+
+@pytest.mark.gpu
+def test_group_failed_step_aborts_and_refuses(gpu, monkeypatch):
+    """a step that fails after its solves were enqueued (fault injection at step 1) aborts the
+    communicator and leaves the group failed: that step and every later call but info / failed
+    / destroy return MPCQP_ERR_DEVICE; bad arguments before anything is enqueued do not"""
+    import ctypes as C
+
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    from mpcqp.group import Group, unique_id
+    torch = gpu
+    monkeypatch.setenv("MPCQP_GROUP_INJECT_FAIL", "1")
+    p = mpcqp.model_params("B")
+    batch = mpcqp.make_batch(p, 16 * 8, seed=3)
+    grp = Group(p, rank=(0, 1, 0, unique_id()))
+    eng = BatchEngine.wrap(p, grp.ctx(0), 0)
+    d = eng.upload(batch)
+    best = torch.zeros(1 + eng.nV, dtype=torch.int64, device="cuda:0")
+    L = mpcqp.lib()
+    # a bad argument (no contact for the SRBM model): refused up front, the group unchanged
+    bad = dict(d, base=0, contact=None)
+    with pytest.raises(RuntimeError):
+        grp.solve_select([bad], [best])
+    assert not grp.failed
+    grp.solve_select([dict(d, base=0)], [best])  # step 0
+    grp.sync()
+    with pytest.raises(RuntimeError):
+        grp.solve_select([dict(d, base=0)], [best])  # step 1: injected failure
+    assert grp.failed
+    with pytest.raises(RuntimeError):
+        grp.solve_select([dict(d, base=0)], [best])
+    assert L.mpcqp_group_wait(grp.g) == 5 and L.mpcqp_group_sync(grp.g) == 5
+    loc = C.c_int()
+    assert L.mpcqp_group_info(grp.g, C.byref(loc), None, None) == 0 and loc.value == 1
+    eng.close()
+    grp.close()

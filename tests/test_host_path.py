@@ -131,3 +131,58 @@ def test_host_tick_overflow_flips(gpu):
         else:
             same(host_solve(eng, p, mixed), ref_m)
     eng.close()
+
+
+def _locked(arrs, fn):
+    """mpcqp_host_register / _unregister over numpy arrays (the caller's own buffers)"""
+    from mpcqp._lib import lib
+    for a in arrs:
+        r = getattr(lib(), fn)(C.c_void_p(a.ctypes.data), *([C.c_size_t(a.nbytes)] if fn.endswith("_register") else []))
+        assert r == 0, (fn, r)
+
+
+@pytest.mark.parametrize("B,gait", [(4096, "alternating"), (40960 + 48, "alternating"),
+                                    (20480, "mixed")])
+def test_host_direct_path_equals_device_path(gpu, B, gait):
+    """page-locked caller arrays (mpcqp_host_register) and B >= 4,096: the direct path (DMA
+    straight from / into the caller's arrays, chunks of >= 8,192 pipelined over three streams;
+    40,960 + 48 instances: a ragged last chunk; the mixed gait: the overflow launch per chunk)
+    equals the device path bit for bit, and so does the staged path of the same context once
+    the arrays are unregistered"""
+    from mpcqp._lib import lib
+    import mpcqp
+    from mpcqp.engine import BatchEngine
+    p = mpcqp.model_params("B")
+    b = mpcqp.make_batch(p, B, seed=202 + B, gait=gait)
+    eng = BatchEngine(p)
+    ref = device_solve(eng, b)
+    nV = p["nu"] * p["N"]
+    ins = [np.ascontiguousarray(b[k]) for k in ("x0", "xref", "lin", "contact")]
+    out = dict(U=np.full(B * nV, np.nan), cost=np.full(B, np.nan), status=np.full(B, 99, np.int32),
+               iters=np.full(B, -1, np.int32))
+    locked = ins + list(out.values())
+    _locked(locked, "mpcqp_host_register")
+    ptr = lambda a: C.c_void_p(a.ctypes.data)
+    for _ in range(2):
+        for v in out.values():
+            v.fill(0)
+        rc = lib().mpcqp_batch_solve_host(eng.ctx, B, *[ptr(a) for a in ins],
+                                          *[ptr(out[k]) for k in ("U", "cost", "status", "iters")])
+        assert rc == 0
+        got = dict(out, U=out["U"].reshape(B, nV))
+        same(got, ref)
+    _locked(locked, "mpcqp_host_unregister")
+    same(host_solve(eng, p, b), ref)
+    eng.close()
+
+
+def test_host_alloc_roundtrip(gpu):
+    """mpcqp_host_alloc / _free: page-locked memory from the library, usable as a host array"""
+    from mpcqp._lib import lib
+    pv = C.c_void_p()
+    assert lib().mpcqp_host_alloc(C.c_size_t(1 << 20), C.byref(pv)) == 0 and pv.value
+    buf = (C.c_double * (1 << 17)).from_address(pv.value)
+    buf[0], buf[-1] = 1.5, -2.5
+    assert buf[0] == 1.5 and buf[-1] == -2.5
+    assert lib().mpcqp_host_free(pv) == 0
+    assert lib().mpcqp_host_free(None) == 6 and lib().mpcqp_host_register(None, 8) == 6

@@ -52,6 +52,10 @@ case "$NAME" in
         timeout -k 10 300 python3 bench.py --global-batch $g --no-per-config --no-host-path \
           --no-cpu-baseline > gpurun_out/${T}_b$g.json || exit 1
       done; } > gpurun_out/${T}.txt 2>&1 ;;
+  smalltrace) # kernel trace of the shard sweep: the GPU's own durations at small shards
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $PWD/gpurun_out/${T}_st -o run \
+      --output-format csv -- python3 tools/shard_sweep.py --sizes 512,2048,4096,8192,65536 --reps 40 \
+      > gpurun_out/${T}_st.log 2>&1 ;;
   stall)      # stall / issue profiles: headline B, config C, config E
     bash tools/pmc_stall.sh gpurun_out/st_$T/B &&
     bash tools/pmc_stall.sh gpurun_out/st_$T/C --driver "tools/time_kernel.py --configs C --batch 65536 --reps 5" &&
