@@ -26,6 +26,9 @@ namespace mpcqp {
 struct FastKernels {
     const void *mpc_gen = nullptr;
     const void *pair = nullptr, *pair_gen = nullptr;  // two QPs per wave (nf <= 30)
+    // the same at a 4-wave register budget, used from pair_w4_min instances per launch
+    const void *pair_w4 = nullptr, *pair_gen_w4 = nullptr;
+    int pair_w4_min = 0;
     size_t pair_lds = 0;
     const void *wg = nullptr;  // workgroup per QP for the overflow list (nf <= 6N)
     size_t wg_lds = 0;
@@ -44,6 +47,12 @@ struct FastKernels {
 };
 
 constexpr int kPairCap = 30;  // free variables of one half of the paired kernel (mpc_pair.hpp)
+// batches from which the paired kernel runs at its 4-wave register budget (fast_pair.hip): below,
+// fewer than ~3 waves per SIMD are resident and the 3-wave build's shorter chain wins
+#ifndef MPCQP_PAIR_W4_MIN
+#define MPCQP_PAIR_W4_MIN 16384
+#endif
+constexpr int kPairW4Min = MPCQP_PAIR_W4_MIN;
 
 // per-family pickers (one translation unit each); false = not instantiated
 bool pick_fast_srbm10(bool fric, int nfmax, FastKernels &k);

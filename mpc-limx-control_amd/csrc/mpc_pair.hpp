@@ -36,9 +36,16 @@ namespace mpcqp {
 
 // LDS loads in flight per step of the unrolled sweeps (a code-motion fence every PF elements):
 // larger hides more LDS latency behind the FMAs, smaller bounds the registers the loads hold
-#ifndef MPCQP_PF_DUAL
-#define MPCQP_PF_DUAL 8
+// (the kernel comes in two register budgets, W = 3 and 4 waves per SIMD (fast_pair.hip); the
+//  4-wave build keeps fewer LDS loads in flight per fence: PFD overrides both)
+template <int W>
+constexpr int pair_pf() {
+#ifdef MPCQP_PF_DUAL
+    return MPCQP_PF_DUAL;
+#else
+    return W >= 4 ? 4 : 8;
 #endif
+}
 // Cholesky + inverse: columns per LDS round trip, and the fence period of its trailing update
 // pair instances by contact schedule within aligned groups of 16 (see pair_sorted_instance)
 #ifndef MPCQP_PAIR_SORT
@@ -77,6 +84,17 @@ namespace mpcqp {
 #endif
 
 constexpr int kPairNF = 30;  // free variables per instance; lane 31 of a half carries g
+
+// a code-motion fence inside an unrolled dot product over an LDS buffer, with the four partial
+// sums pinned in registers: the compiler can neither hoist the later loads above it nor sink the
+// FMAs below it, so at most one fence period of loads is in flight (the loops' register peak)
+__device__ __forceinline__ void pin_fence4(double (&s4)[4]) {
+    pin(s4[0]);
+    pin(s4[1]);
+    pin(s4[2]);
+    pin(s4[3]);
+    step_fence();
+}
 // crash start (below): bounds per working set, working sets before giving up
 #ifndef MPCQP_CRASH_K
 #define MPCQP_CRASH_K 12
@@ -95,8 +113,12 @@ struct PairLayout {
     static constexpr int HB = NF * (NF + 1) / 2;     // packed H_FF
     // doubles; one region, in turn:
     //   early   : X0, X1 support rows, A x0, A^2 x0, xref, x0, then u_m / v_m   [oU, eUV)
-    //   H build : packed H [oU, oU + HB) over the dead early view; S and the R copy after it
-    //   solver  : packed L / R [oU, oU + NR), then 5 x 32 broadcast doubles
+    //   H build : packed H [oU, oU + HB) over the dead early view; S after it (R and the Q / P
+    //             diagonals are read from global memory, not staged per instance)
+    //   solver  : packed R^-1 [oU, oU + HB) (crash: the published J rows), then the broadcast
+    //             buffers over the dead S: buf | colb | rot (2 NP) | a zero slot
+    // then bytes: the parked contact mask and instance index, the free map (int8: fid[NF],
+    // pos[NV]).  5 KB per instance at config B: 16 waves (32 instances) fit a CU's 160 KB.
     static constexpr int oU = 0;
     static constexpr int oX0 = oU;                       // [NU][SD]
     static constexpr int oX1 = oX0 + NU * SD;            // [NU][SD]
@@ -107,19 +129,23 @@ struct PairLayout {
     static constexpr int oUV = oX0v + NX;                // [(N+1)][2][NU]
     static constexpr int eUV = oUV + (N + 1) * 2 * NU;
     static constexpr int oS = oU + ((HB > eUV - oU ? HB : eUV - oU) + 1) / 2 * 2;  // [NU*NU][4]
-    static constexpr int oRm = oS + 4 * NU * NU;         // R (NU x NU)
-    static constexpr int oWq = oRm + NU * NU;            // diag Q, diag P (NX each)
-    static constexpr int eMid = oWq + 2 * NX;
+    static constexpr int eMid = oS + 4 * NU * NU;
     static constexpr int oR = oU;
-    static constexpr int oRow = (oR + NR + 1) & ~1;      // buf | colb | rot (2 NP) | 1/R(j,j)
-    static constexpr int eLate = oRow + 5 * NP;
-    static constexpr int oCt = ((eMid > eLate ? eMid : eLate) + 1) & ~1;  // contact mask (u64)
-    static constexpr int oDump = oCt + 2;  // sink of the H build's masked-off stores
-    static constexpr int nDoubles = oDump + 1;
-    static constexpr size_t bytes =
-        (sizeof(double) * nDoubles + sizeof(int) * (NF + NV) + 15) & ~(size_t)15;
+    static constexpr int oDump = oU + HB;  // sink of the H build's masked-off stores (past H)
+    // R^-1 packed needs HB doubles; the R form of the A/B build (MPCQP_PAIR_RINV=0) NR, with its
+    // 1/R(j,j) buffer after the rotations
+    static constexpr int oRow = (oR + (MPCQP_PAIR_RINV ? HB : NR) + 1) & ~1;  // buf | colb | rot
+    // (+ 2: the dual loop's zero slot and the crash's objective slot)
+    static constexpr int eLate = oRow + 4 * NP + (MPCQP_PAIR_RINV ? 2 : NP + 2);
+    static constexpr int nDoubles = ((eMid > eLate ? eMid : eLate) + 1) & ~1;
+    static constexpr size_t oCt = sizeof(double) * nDoubles;  // u64 contact mask, int64 index
+    static constexpr size_t oFid = oCt + 16;                  // int8 [NF]: variable of slot p
+    static constexpr size_t oPos = oFid + NF;                 // int8 [NV]: slot of variable v
+    static constexpr size_t bytes = (oPos + NV + 15) & ~(size_t)15;
     static constexpr size_t lds_bytes = 2 * bytes;  // both halves
     static_assert(oU % 2 == 0 && oRow % 2 == 0 && oS % 2 == 0, "16-byte aligned buffers");
+    static_assert(oDump < oRow && oDump >= eUV, "the dump slot is free during the H build");
+    static_assert(NV < 128 && NF < 128, "int8 free map");
     static_assert(HB <= NR, "packed H fits the L / R space");
     static_assert(NV <= NR, "the U staging row fits the L / R space");
     static_assert(N <= kHalf, "one lane per horizon step in the gait mask");
@@ -273,18 +299,20 @@ __device__ __forceinline__ void fold_trailing_k(double (&s)[NF], int k, double A
 // textbook flops of one crash working-set solve with k bounds and of one dual pass with q
 // constraints active, nf free variables (mpcqp/flops.py, the oracle's t_sflops): the diagnostic
 // solver-flops counter (MpcArgs::flops_acc)
-__device__ __forceinline__ double crash_ws_flops_d(int nf, int k) {
-    const double f = nf, kk = k;
-    return kk * (kk + 1.0) * f + (kk - 1.0) * kk * (kk + 1.0) + 2.0 * kk * f + 2.0 * f * f + f +
-           3.0 * kk;
+// (integers: a half's total stays far below 2^31 -- at most max_iter passes of ~6 k each)
+__device__ __forceinline__ int crash_ws_flops_i(int nf, int k) {
+    return k * (k + 1) * nf + (k - 1) * k * (k + 1) + 2 * k * nf + 2 * nf * nf + nf + 3 * k;
 }
-__device__ __forceinline__ double pass_flops_d(int nf, int q) {
-    const double f = nf, qq = q, r = nf > q ? (double)(nf - q) : 0.0;
-    return qq * qq + 4.0 * f + 6.0 * f * r + 2.0 * f + 3.0 * qq;
+__device__ __forceinline__ int pass_flops_i(int nf, int q) {
+    const int r = nf > q ? nf - q : 0;
+    return q * q + 4 * nf + 6 * nf * r + 2 * nf + 3 * q;
 }
 
-template <int NU, int N, int MODEL, bool GEN>
+template <int NU, int N, int MODEL, bool GEN, int W>
 __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) {
+    // loads in flight per code-motion fence in the unrolled dot products over LDS buffers:
+    // more hides more LDS latency, fewer bounds the registers the loads hold
+    constexpr int PFD = pair_pf<W>(), PFG = pair_pf<W>();
     static_assert(!GEN || MODEL == 0, "generated inputs are defined for the SRBM model");
     static_assert(MODEL == 0 || MODEL == 1, "TRON1 models only");
     using Lay = PairLayout<NU, N, MODEL>;
@@ -298,12 +326,15 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     const bool valid = bq < a.B;
     const int b = valid ? bq : a.B - 1;  // the spare half of an odd batch re-reads the last QP
     [[maybe_unused]] const int b_ = b;
-    double *D = reinterpret_cast<double *>(smem + (up ? Lay::bytes : 0));
-    int *fid = reinterpret_cast<int *>(D + Lay::nDoubles);
-    int *pos = fid + NF;
+    unsigned char *Dbase = smem + (up ? Lay::bytes : 0);
+    double *D = reinterpret_cast<double *>(Dbase);
+    signed char *fid = reinterpret_cast<signed char *>(Dbase + Lay::oFid);
+    signed char *pos = reinterpret_cast<signed char *>(Dbase + Lay::oPos);
     double *X0 = D + Lay::oX0, *X1 = D + Lay::oX1, *Ax = D + Lay::oAx, *A2x = D + Lay::oA2x;
     double *xr = D + Lay::oXr, *x0g = D + Lay::oX0v, *UV = D + Lay::oUV;
-    double *S = D + Lay::oS, *Rm = D + Lay::oRm, *Wq = D + Lay::oWq;
+    double *S = D + Lay::oS;
+    const double *Rm = a.rmat;  // R (NU x NU) and the Q / P diagonals: global, L1/L2-resident
+    const double *Qd = a.qd, *Pd = a.pd;
 
     // ---- per-instance inputs: all global loads back to back, then parked in LDS
     double lin[8];
@@ -318,13 +349,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         for (int i = 0; i < 6; ++i) lin[1 + i] = a.feet[(size_t)s_ * 6 + i];
         lin[7] = 0.0;
         const double ph0 = a.phase[b];
-        const double rm0 = (hl < NRM) ? a.rmat[hl] : 0.0;
-        const double rm1 = (hl + kHalf < NRM) ? a.rmat[hl + kHalf] : 0.0;
-        const double wq = (hl < 2 * NX) ? (hl < NX ? a.qd[hl] : a.pd[hl - NX]) : 0.0;
-        if (hl < 2 * NX) Wq[hl] = wq;
         if (hl < NX) x0g[hl] = stv;
-        if (hl < NRM) Rm[hl] = rm0;
-        if (hl + kHalf < NRM) Rm[hl + kHalf] = rm1;
         lin[0] = hbcast<2>(stv);
         if (hl < NX) {
 #pragma unroll
@@ -353,17 +378,11 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
 #pragma unroll
         for (int r = 0; r < RX; ++r) v[r] = (hl + r * kHalf < NXR) ? stream_load(xrg + hl + r * kHalf) : 0.0;
         const double x0l = (hl < NX) ? stream_load(a.x0 + (size_t)b * NX + hl) : 0.0;
-        const double rm0 = (hl < NRM) ? a.rmat[hl] : 0.0;
-        const double rm1 = (hl + kHalf < NRM) ? a.rmat[hl + kHalf] : 0.0;
-        const double wq = (hl < 2 * NX) ? (hl < NX ? a.qd[hl] : a.pd[hl - NX]) : 0.0;
         if (MODEL == 0) contact = stream_load(a.contact + b);
 #pragma unroll
         for (int r = 0; r < RX; ++r)
             if (hl + r * kHalf < NXR) xr[hl + r * kHalf] = v[r];
         if (hl < NX) x0g[hl] = x0l;
-        if (hl < 2 * NX) Wq[hl] = wq;
-        if (hl < NRM) Rm[hl] = rm0;
-        if (hl + kHalf < NRM) Rm[hl + kHalf] = rm1;
     }
     wave_sync();
     MPCQP_CUT(a.cut, 11);
@@ -390,7 +409,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         if (nf > NF) status = ST_BAD_DIMS;
     }
     if (nf > a.max_free) status = ST_BAD_DIMS;
-    uint64_t *ctl = reinterpret_cast<uint64_t *>(D + Lay::oCt);
+    uint64_t *ctl = reinterpret_cast<uint64_t *>(Dbase + Lay::oCt);
     if (hl == 0) {  // reloaded for the outputs: nothing per instance stays live
         ctl[0] = contact;
         ctl[1] = (uint64_t)(valid ? bq : -1);
@@ -510,7 +529,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             const int r_ = blk & 1, w_ = blk >> 1;
             const int lo = r_ ? Sup::x1lo : Sup::x0lo;
             const double *Xr = r_ ? X1 : X0;
-            const double *w = Wq + (w_ ? NX : 0);  // diag P / Q staged in LDS
+            const double *w = w_ ? Pd : Qd;  // diag P / Q (uniform addresses: scalar loads)
             for (int e = hl; e < NRM; e += kHalf) {
                 const int ci = e % NU, cj = e / NU;
                 double acc = 0.0;
@@ -528,7 +547,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             const int m = 1 + e / NSUP, t = e % NSUP;
             const int l = t < SD ? Sup::x1lo + t : Sup::x0lo + t - SD;
             const double md = (double)m, hm2 = 0.5 * md * md;
-            const double wl = Wq[(m < N ? 0 : NX) + l];
+            const double wl = (m < N ? Qd : Pd)[l];
             xr[m * NX + l] = wl * (x0g[l] + md * Ax[l] + hm2 * A2x[l] - xr[m * NX + l]);
         }
         wave_sync();
@@ -552,7 +571,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     // the batch: B standing's every wavefront) goes straight to the outputs
     double fval = 0.0, x = 0.0;
     int iters = 0;
-    double sfl = 0.0;  // this half's solver flops (diagnostic counter, MpcArgs::flops_acc)
+    int sfl = 0;  // this half's solver flops (diagnostic counter, MpcArgs::flops_acc)
     if (work) {
         // ---- g (lane p: g_p), then H_FF over the dead early view (lane p loads row p)
         const bool ok = valid && status == ST_OK && nf > 0;
@@ -717,11 +736,12 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             //      row throughout) and ends with t = L^-1 g.  One FMA per (step, slot) instead of the
             //      fused sweep's two (one for H, one for J); the two triangles of the square the lanes
             //      swept are one triangle each, and the J array costs no registers of its own.
-            static_assert(Lay::oRow == Lay::oR + lrow(kHalf - 1), "row 31 (g) is the row buffer");
+            // (lane 31 reads g from the row buffer: its row of the padded matrix)
             if (hl < NF) rowbuf[hl] = gv;
             wave_sync();
             {
-                const double *Hr = D + Lay::oR + lrow(hl), *Hc = D + Lay::oR + hl;
+                const double *Hr = hl == kHalf - 1 ? rowbuf : D + Lay::oR + lrow(hl),
+                             *Hc = D + Lay::oR + hl;
     #pragma unroll
                 for (int q = 0; q < NF; ++q) {
                     if (MPCQP_FOLD_ASEL) {  // one load from the selected address
@@ -736,7 +756,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             static_assert(MPCQP_CHOL_CB == 2, "the folded sweep runs column pairs");
             double *dg = rot;  // pivot of every column (uniform stores), for the final scaling
             double piv = hbcast<0>(Jr[0]);
-            bool bad = !(piv > 0.0);
+            int bad = !(piv > 0.0);  // (an int pinned every step: see below)
             double ik = rsqrt_nr(piv);
     #pragma unroll
             for (int k = 0; k < NF; k += 2) {
@@ -751,7 +771,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 row_pair(m0, A0, B0);  // the column's rows 0-15 / 16-31 in every row of the half
                 fold_in_panel<NF>(Jr, A0, B0, m0, k);  // slot k + 1 -= L(k + 1, k) m0
                 const double pc = hbcast(Jr[k + 1], k + 1);
-                bad |= !(pc > 0.0);
+                bad |= !(pc > 0.0) ? 1 : 0;
                 const double ik1 = rsqrt_nr(pc);
                 Jr[k + 1] *= ik1;
                 const bool own1 = hl == k + 1;
@@ -764,7 +784,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                     double hn = Jr[k + 2 < NF ? k + 2 : k];
                     hn -= Jr[k] * Jr[k];
                     pivn = hbcast(hn - Jr[k + 1] * Jr[k + 1], k + 2);
-                    bad |= !(pivn > 0.0);
+                    bad |= !(pivn > 0.0) ? 1 : 0;
                     ikn = rsqrt_nr(pivn);
                 }
                 dg[k] = pk;
@@ -779,6 +799,9 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 ik = ikn;
                 pin(piv);
                 pin(ik);
+                // the non-PD test is evaluated here, each step: left to the compiler, every
+                // column's pivot stayed live to a test sunk after the sweep (60 VGPRs)
+                asm volatile("" : "+v"(bad));
                 step_fence();
             }
             {   // rows of J: slots >= l times -1 / piv_l, the L row below zeroed; lane 31 keeps t
@@ -788,7 +811,11 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 const double cl = gl ? 1.0 : -1.0 / pl;
                 const int lim = gl ? 0 : (hl < NF ? hl : NF);
     #pragma unroll
-                for (int j = 0; j < NF; ++j) Jr[j] = (j < lim) ? 0.0 : Jr[j] * cl;
+                for (int j = 0; j < NF; ++j) {
+                    Jr[j] = (j < lim) ? 0.0 : Jr[j] * cl;
+                    pin(Jr[j]);  // (in place: the scaled row does not take a second register set)
+                    if ((j & 7) == 7) step_fence();
+                }
             }
 #else
             // ---- Cholesky fused with the inverse sweep.  Right-looking, lane l owns row l of H_FF
@@ -901,7 +928,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     #pragma unroll
             for (int j = 0; j < NF; ++j) {
                 s4[j & 3] += Jr[j] * colb[j];
-                if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
+                if ((j % PFD) == PFD - 1) pin_fence4(s4);
             }
             x = (ok2 && hl < nf) ? -((s4[0] + s4[1]) + (s4[2] + s4[3])) : 0.0;
             fval = half_sum(hl < nf ? gv * gv : 0.0);
@@ -969,14 +996,19 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             constexpr int KC = kPairCrashK, CH = 2;
             static_assert(KC % CH == 0, "whole chunks");
             const int PC = a.crash_p;
-            static_assert(KC * NF <= Lay::NR, "the published J rows fit the dead L space");
+            static_assert(KC * NF <= Lay::HB, "the published J rows fit the dead H space");
             static_assert(KC + 2 <= NP, "the pivot row fits the row buffer");
             double *Wr = D + Lay::oR;             // [KC][NF] published J rows
             double *Pv = rowbuf;                  // pivot row [KC], its r, 1 / pivot
             double *Wv = colb;                    // w by rank
             double *Yv = rot;                     // y = J_A' w [NF]
             const double x0v = x, f0 = fval;
-            double xc = x0v, lam = 0.0, fc = f0;
+            double xc = x0v;
+            // the objective at xc (uniform per half) is parked in LDS: a register pair less
+            // through the Gram and Gauss-Jordan, the crash's register peak
+            double *fcs = D + Lay::oRow + 4 * NP + 1;
+            if (hl == 0) *fcs = f0;
+            bool lneg = false;  // this bound's multiplier is negative (dropped next)
             int side = 0, cit = 0;
             bool crashing = !done, cok = false;
             while (__ballot(crashing) != 0ull) {
@@ -987,7 +1019,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                     if (side == 0) {
                         if ((stb & 1) && xc - MPCQP_BLO < MPCQP_TLO) nw = 1;
                         else if ((stb & 2) && -xc - MPCQP_BHI < MPCQP_THI) nw = -1;
-                    } else if (lam < 0.0) {
+                    } else if (lneg) {
                         nw = 0;
                     }
                 }
@@ -1009,15 +1041,13 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 const int rho = __popc(amask & ((1u << hl) - 1u));
                 const bool solving = crashing && k > 0;
                 const bool inA = solving && side != 0;
-                if (crashing && k == 0) { xc = x0v; lam = 0.0; fc = f0; }
+                if (crashing && k == 0) { xc = x0v; lneg = false; if (hl == 0) *fcs = f0; }
                 if (solving) ++iters;
-                if (a.flops_acc && solving) sfl += crash_ws_flops_d(nf, k);
+                if (a.flops_acc && solving) sfl += crash_ws_flops_i(nf, k);
                 const int ks = solving ? k : 0;
                 const int kmax = max(__builtin_amdgcn_readlane(ks, 0), __builtin_amdgcn_readlane(ks, kHalf));
                 if (kmax == 0) continue;  // (wave-uniform)
-                const double bval = side > 0 ? MPCQP_BLO : -MPCQP_BHI;
-                const double r0 = x0v - bval;
-                double rr = r0;
+                double rr = x0v - (side > 0 ? MPCQP_BLO : -MPCQP_BHI);
                 if (inA) {
         #pragma unroll
                     for (int c = 0; c < NF; ++c) Wr[rho * NF + c] = Jr[c];
@@ -1034,7 +1064,11 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                         for (int c = 0; c < NF; ++c) {
         #pragma unroll
                             for (int m = 0; m < CH; ++m) Mr[m0 + m] += Jr[c] * Wr[(m0 + m) * NF + c];
-                            if ((c % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
+                            if ((c % PFG) == PFG - 1) {
+        #pragma unroll
+                                for (int m = 0; m < CH; ++m) pin(Mr[m0 + m]);
+                                step_fence();
+                            }
                         }
                     }
                 }
@@ -1065,26 +1099,32 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                         }
                         wave_sync();
                         const double pr = Pv[KC], pi = Pv[KC + 1];
-                        double pv[KC];
+                        const bool upd = inA && rho != j && j < k;
+                        const double l = Mr[j] * pi;
+                        // the pivot row in chunks of four (loads outside the divergent update,
+                        // at most one chunk of it in registers)
         #pragma unroll
-                        for (int m = j + 1; m < KC; ++m) pv[m] = Pv[m];
-                        if (inA && rho != j && j < k) {
-                            const double l = Mr[j] * pi;
+                        for (int m0 = (j + 1) & ~3; m0 < KC; m0 += 4) {
+                            if (m0 < kmax) {
+                                double pv[4];
         #pragma unroll
-                            for (int m0 = (j + 1) & ~3; m0 < KC; m0 += 4) {
-                                if (m0 < kmax) {
+                                for (int m = m0; m < m0 + 4; ++m) pv[m - m0] = m > j ? Pv[m] : 0.0;
+                                if (upd) {
         #pragma unroll
                                     for (int m = m0; m < m0 + 4; ++m)
-                                        if (m > j) Mr[m] -= l * pv[m];
+                                        if (m > j) Mr[m] -= l * pv[m - m0];
                                 }
                             }
-                            rr -= l * pr;
                         }
+                        if (upd) rr -= l * pr;
                     }
                 }
                 const bool gave_up = half_ballot(bad) != 0u;
                 const double w = inA ? rr / dd : 0.0;
                 if (inA) Wv[rho] = w;
+                // (b and the right-hand side re-derived after the elimination: not live through it)
+                const double bval = side > 0 ? MPCQP_BLO : -MPCQP_BHI;
+                const double wr = half_sum(inA ? w * (x0v - bval) : 0.0);
                 wave_sync();
                 // y = J_A' w (lane c: column c of the published rows), then x = x0 - J y
                 double yv[CH] = {};
@@ -1106,20 +1146,23 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 wave_sync();
                 double s4[4] = {0.0, 0.0, 0.0, 0.0};
         #pragma unroll
-                for (int c = 0; c < NF; ++c) s4[c & 3] += Jr[c] * Yv[c];
-                const double wr = half_sum(inA ? w * r0 : 0.0);
+                for (int c = 0; c < NF; ++c) {
+                    s4[c & 3] += Jr[c] * Yv[c];
+                    if ((c % PFD) == PFD - 1) pin_fence4(s4);
+                }
                 wave_sync();
                 if (solving && !gave_up) {
                     xc = hl < nf ? x0v - ((s4[0] + s4[1]) + (s4[2] + s4[3])) : 0.0;
                     if (inA) xc = bval;
-                    lam = inA ? -(double)side * w : 0.0;
-                    fc = f0 + 0.5 * wr;
+                    lneg = inA && -(double)side * w < 0.0;
+                    if (hl == 0) *fcs = f0 + 0.5 * wr;
                 }
                 if (solving && gave_up) crashing = false;
             }
+            wave_sync();
             if (cok) {  // this half is solved: the dual loop skips it
                 x = xc;
-                fval = fc;
+                fval = *fcs;
                 done = true;
             }
         }
@@ -1186,7 +1229,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             const bool stepping = go && !done;
             if (stepping) {
                 ++iters;
-                if (a.flops_acc) sfl += pass_flops_d(nf, q);
+                if (a.flops_acc) sfl += pass_flops_i(nf, q);
                 // |d(0:q)|^2 and |d(q+1:nf)|^2 in one two-sum pass; zn = |d2|^2 = zq + d_q^2 and
                 // dd = |d|^2 = zn + the first part
                 double sq = hl < q ? dj * dj : 0.0;
@@ -1199,7 +1242,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     #pragma unroll
                 for (int j = 0; j < NF; ++j) {
                     z4[j & 3] += Jr[j] * rowbuf[j];
-                    if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
+                    if ((j % PFD) == PFD - 1) pin_fence4(z4);
                 }
                 z = sg * ((z4[0] + z4[1]) + (z4[2] + z4[3]));
                 pin(z);  // here, not sunk to its use after the R solve: the row would stay live
@@ -1400,13 +1443,13 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     #pragma unroll
                 for (int j = 0; j < NF; ++j) {
                     w4[j & 3] += Jr[j] * rowbuf[j];
-                    if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
+                    if ((j % PFD) == PFD - 1) pin_fence4(w4);
                 }
                 const double f = hh ? beta * ((w4[0] + w4[1]) + (w4[2] + w4[3])) : 0.0;
     #pragma unroll
                 for (int j = 0; j < NF; ++j) {
                     Jr[j] -= f * rowbuf[j];
-                    if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
+                    if ((j % PFD) == PFD - 1) step_fence();
                 }
             }
             if (__ballot(rt) != 0ull) {
@@ -1421,7 +1464,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                     const double y0 = Jr[j], y1 = Jr[j + 1];
                     Jr[j] = c * y0 + s_ * y1;
                     Jr[j + 1] = -s_ * y0 + c * y1;
-                    if ((j % MPCQP_PF_DUAL) == MPCQP_PF_DUAL - 1) step_fence();
+                    if ((j % PFD) == PFD - 1) step_fence();
                 }
             }
             wave_sync();
@@ -1447,8 +1490,10 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     asm volatile("" : "+v"(lno));
     const int hlo = lno & (kHalf - 1);
     double *Do = reinterpret_cast<double *>(smem + (lno >= kHalf ? Lay::bytes : 0));
-    const int *fido = reinterpret_cast<const int *>(Do + Lay::nDoubles), *poso = fido + NF;
-    const uint64_t *ctlo = reinterpret_cast<const uint64_t *>(Do + Lay::oCt);
+    const unsigned char *Dob = smem + (lno >= kHalf ? Lay::bytes : 0);
+    const signed char *fido = reinterpret_cast<const signed char *>(Dob + Lay::oFid);
+    const signed char *poso = reinterpret_cast<const signed char *>(Dob + Lay::oPos);
+    const uint64_t *ctlo = reinterpret_cast<const uint64_t *>(Dob + Lay::oCt);
     const int bo = (int)(long long)ctlo[1];
     const bool defer = a.ovf && nf > NF && nf <= a.max_free;  // the workgroup kernel takes it
     {  // one append (one atomic) for the wavefront's deferred instances
@@ -1482,7 +1527,8 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         }
     }
     if (a.flops_acc) {  // (diagnostic) both halves' solver flops, one atomic per wavefront
-        const double t = readlane(sfl, 0) + readlane(sfl, kHalf);
+        const double t = (double)__builtin_amdgcn_readlane(sfl, 0) +
+                         (double)__builtin_amdgcn_readlane(sfl, kHalf);
         if (lno == 0) atomicAdd(a.flops_acc + (blockIdx.x % kFlopsSlots) * kFlopsStride, t);
     }
 #ifndef MPCQP_FUSED_SEL

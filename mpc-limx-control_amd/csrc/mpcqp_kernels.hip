@@ -448,6 +448,12 @@ bool pick_fast(int model, int nx, int nu, int N, bool fric, int nfmax, FastKerne
     // working sets (0: the plain dual loop from the unconstrained minimum; A/B runs and tests)
     if (k.pair && k.crash_k > 0)
         if (const char *e = getenv("MPCQP_CRASH_P")) k.crash_p = std::max(0, atoi(e));
+    // the 4-wave build from this many instances per launch (MPCQP_PAIR_W4_MIN=n: A/B and tests;
+    // 0 = never)
+    if (k.pair) {
+        k.pair_w4_min = kPairW4Min;
+        if (const char *e = getenv("MPCQP_PAIR_W4_MIN")) k.pair_w4_min = std::max(0, atoi(e));
+    }
     // (diagnostic MPCQP_PAIR_LDS_PAD=bytes: extra LDS per paired-kernel wave, i.e. fewer resident
     //  waves per CU -- the kernel's occupancy sensitivity, tools/ab_env.py; never in a measured line)
     if (k.pair)
@@ -1360,6 +1366,10 @@ static int launch_mpc(mpcqp_ctx *c, bool gen, int B, MpcArgs *a, bool may_overfl
         a->ovf_cap = ovf_list_cap((long long)c->list_cap);
     }
     const void *pk = gen ? c->fk.pair_gen : c->fk.pair;
+    if (pk && B >= c->fk.pair_w4_min && c->fk.pair_w4_min > 0) {
+        const void *p4 = gen ? c->fk.pair_gen_w4 : c->fk.pair_w4;
+        if (p4) pk = p4;
+    }
     a->sel_final = a->ovf ? 0 : 1;  // fused selection: the batch's last launch finalizes
     if (a->flops_acc && pk) ++c->flops_launches;
     tbegin(c, 2);
