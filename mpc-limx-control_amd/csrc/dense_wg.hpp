@@ -224,6 +224,7 @@ __device__ __forceinline__ void dense_mpc_one(const MpcArgs &a, int b, unsigned 
     });
     __syncthreads();
     MPCQP_STAMP(a.stamps, 11, tst);
+    MPCQP_CUT(a.cut, 91);  // (cuts build: inputs + expm + free map)
 
     double hr[NH];
 #pragma unroll
@@ -291,6 +292,7 @@ __device__ __forceinline__ void dense_mpc_one(const MpcArgs &a, int b, unsigned 
         nf = C.nf;
         ok = C.status == ST_OK && nf > 0;
         MPCQP_STAMP(a.stamps, 4, tst);
+        MPCQP_CUT(a.cut, 92);  // (cuts build: + [Phi | X], Psi, gradient)
         // ---- H rows: rounds of two row tiles (rho, TR-1-rho): their 16 I + 16 tiles of G' G
         //      over the waves, staged (rows of I at stg, of I' after them), then every thread
         //      takes H(r, c) = 2 (G'G(r, c) + R(c_c, c_r) [k_r == k_c]), c = 2j + h <= r
@@ -479,6 +481,7 @@ __device__ __forceinline__ void dense_mpc_one(const MpcArgs &a, int b, unsigned 
     const double g = (ok && r < nf) ? fv[C.L.fid[r]] : 0.0;
     __syncthreads();  // the solver's workspace overlays the front
     MPCQP_STAMP(a.stamps, 3, tst);
+    MPCQP_CUT(a.cut, 93);  // (cuts build: + the H rows)
     gi_run_wg<NF, true>(C, hr, g, D + Lay::oU);
     MPCQP_STAMP_INIT(tw);
     SolveOut O;

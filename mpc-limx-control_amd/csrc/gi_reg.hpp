@@ -18,6 +18,7 @@
 // constant lane indices.
 #pragma once
 #include "chol_reg.hpp"
+#include "gi_crash_reg.hpp"
 #include "gi_solver.hpp"
 
 namespace mpcqp {
@@ -315,6 +316,21 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
 #pragma unroll
             for (int t = 0; t < 4; ++t)
                 if (warm_bit(w, fb + t)) gmask |= 4 << t;
+        }
+    }
+// (off: on config C's friction problems the primal-dual iteration stalls on the degenerate
+//  pyramid apex of unloaded feet -- tools/crash_sim_friction.py: even the optimum's own active
+//  set converges for 209 of 256 instances, the rest cycle -- so the rollouts measured 1.03x the
+//  cold loop's iterations with it against 0.89x without)
+#ifndef MPCQP_REG_WARM_CRASH
+#define MPCQP_REG_WARM_CRASH 0
+#endif
+    // warm start: the seeded set solved in one working-set step (gi_crash_reg.hpp); the dual
+    // loop below runs only if that start gives up (then exactly as without it)
+    if constexpr (RegCrashLayout<NF>::end <= RegPack<NF>::doubles) {  // (NF = 60, 64)
+        if (MPCQP_REG_WARM_CRASH && warm && !done && __ballot(gmask != 0) != 0ull) {
+            if (reg_warm_crash<NF>(C, Jr, fbase, gmask, x, fval, iters, L.R)) done = true;
+            gmask = 0;  // (after a give-up the dual loop runs cold)
         }
     }
     MPCQP_SUB_INIT(tsub);

@@ -191,29 +191,41 @@ __device__ __forceinline__ int row_bcast_u32(int v, int j) {
         default: return 0;
     }
 }
-template <bool GEN>
+template <bool GEN, int N>
 __device__ __forceinline__ int pair_sorted_instance(const MpcArgs &a) {
     const int ln = lane(), c = ln & 15;
     const int wv = xcd_order((int)blockIdx.x, (int)gridDim.x);
     const int g0 = (2 * wv) & ~15;
     const int gn = a.B - g0 < 16 ? a.B - g0 : 16;
-    unsigned long long key = ~0ull;
-    if (c < gn) {
-        if constexpr (GEN) {
-            const double cyc = (double)(a.swing + a.stance);
-            key = (unsigned long long)__double_as_longlong(fmod(a.phase[g0 + c], cyc));
-        } else {
-            key = a.contact[g0 + c];
-        }
-    }
-    const int klo = (int)(key & 0xffffffffull), khi = (int)(key >> 32);
     int rank = 0;
+    if constexpr (!GEN && 2 * N <= 32) {
+        // the schedule's bits (2k + foot, k < N) fit 32 bits: one DPP move and one compare per
+        // candidate (bits above 2N, if a caller sets any, only change the pairing, never a result)
+        unsigned key = ~0u;
+        if (c < gn) key = (unsigned)a.contact[g0 + c];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {  // row_newbcast: key j of this 16-lane row
-        const unsigned lo = (unsigned)row_bcast_u32(klo, j);
-        const unsigned hi = (unsigned)row_bcast_u32(khi, j);
-        const unsigned long long kj = ((unsigned long long)hi << 32) | lo;
-        rank += (j < gn && (kj < key || (kj == key && j < c))) ? 1 : 0;
+        for (int j = 0; j < 16; ++j) {  // row_newbcast: key j of this 16-lane row
+            const unsigned kj = (unsigned)row_bcast_u32((int)key, j);
+            rank += (j < gn && (kj < key || (kj == key && j < c))) ? 1 : 0;
+        }
+    } else {
+        unsigned long long key = ~0ull;
+        if (c < gn) {
+            if constexpr (GEN) {
+                const double cyc = (double)(a.swing + a.stance);
+                key = (unsigned long long)__double_as_longlong(fmod(a.phase[g0 + c], cyc));
+            } else {
+                key = a.contact[g0 + c];
+            }
+        }
+        const int klo = (int)(key & 0xffffffffull), khi = (int)(key >> 32);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {  // row_newbcast: key j of this 16-lane row
+            const unsigned lo = (unsigned)row_bcast_u32(klo, j);
+            const unsigned hi = (unsigned)row_bcast_u32(khi, j);
+            const unsigned long long kj = ((unsigned long long)hi << 32) | lo;
+            rank += (j < gn && (kj < key || (kj == key && j < c))) ? 1 : 0;
+        }
     }
     // ranks 2w' (lower half) and 2w'+1 (upper half), both read off lanes 0-15 (row 0)
     const int r0 = (2 * wv) & 15;
@@ -322,7 +334,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     const int ln = lane(), hl = ln & (kHalf - 1);
     const bool up = ln >= kHalf;
     int bq = 2 * xcd_order((int)blockIdx.x, (int)gridDim.x) + (up ? 1 : 0);
-    if constexpr (MPCQP_PAIR_SORT && MODEL == 0) bq = pair_sorted_instance<GEN>(a);
+    if constexpr (MPCQP_PAIR_SORT && MODEL == 0) bq = pair_sorted_instance<GEN, N>(a);
     const bool valid = bq < a.B;
     const int b = valid ? bq : a.B - 1;  // the spare half of an odd batch re-reads the last QP
     [[maybe_unused]] const int b_ = b;
@@ -571,6 +583,9 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     // the batch: B standing's every wavefront) goes straight to the outputs
     double fval = 0.0, x = 0.0;
     int iters = 0;
+    // warm start (GEN rollouts, MpcArgs::warm): the lane's bounds active at the end, bit 0 lower,
+    // bit 1 upper, written back for the next tick
+    [[maybe_unused]] int act2 = 0;
     int sfl = 0;  // this half's solver flops (diagnostic counter, MpcArgs::flops_acc)
     if (work) {
         // ---- g (lane p: g_p), then H_FF over the dead early view (lane p loads row p)
@@ -1011,6 +1026,22 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             bool lneg = false;  // this bound's multiplier is negative (dropped next)
             int side = 0, cit = 0;
             bool crashing = !done, cok = false;
+            // warm start (rollouts): the previous tick's active bound of this
+            // variable, one horizon step later (step k now was step k + 1 then; the last step
+            // repeats), joins the FIRST working set even when x0 does not violate it; the
+            // primal-dual iteration then drops it if its multiplier is negative.  The optimum is
+            // the same point (strictly convex QP); only the number of working sets changes.
+            int seed = 0;
+            if constexpr (GEN) {
+                if (a.warm && crashing && hl < nf) {
+                    const int bw = (int)(long long)ctl[1];
+                    const unsigned long long *w = a.warm + (size_t)bw * a.warm_words;
+                    const int v = fid[hl], kv = v / NU, cv = v % NU;
+                    const int vs = (kv + 1 < N ? kv + 1 : kv) * NU + cv;
+                    if (((w[vs >> 6] >> (vs & 63)) & 1ull) && (stb & 1)) seed = 1;
+                    else if (((w[(NV + vs) >> 6] >> ((NV + vs) & 63)) & 1ull) && (stb & 2)) seed = -1;
+                }
+            }
             while (__ballot(crashing) != 0ull) {
                 int nw = side;
                 if (crashing && hl < nf) {
@@ -1019,6 +1050,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                     if (side == 0) {
                         if ((stb & 1) && xc - MPCQP_BLO < MPCQP_TLO) nw = 1;
                         else if ((stb & 2) && -xc - MPCQP_BHI < MPCQP_THI) nw = -1;
+                        else if (GEN && cit == 0) nw = seed;
                     } else if (lneg) {
                         nw = 0;
                     }
@@ -1164,6 +1196,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 x = xc;
                 fval = *fcs;
                 done = true;
+                if constexpr (GEN) act2 = side > 0 ? 1 : (side < 0 ? 2 : 0);
             }
         }
 #endif
@@ -1475,6 +1508,15 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
     #ifdef MPCQP_STAMPS
         if (a.stamps && ln == 0) atomicAdd(&a.stamps[2], npass);
     #endif
+        if constexpr (GEN) {  // the dual loop's final active bounds (stb: bit cleared = active)
+            if (a.warm && ok2 && status == ST_OK && hl < nf) {
+                double lo, hi;
+                pair_bound<NU, MODEL>(a, ~0ull, fid[hl], lo, hi);
+                const int st0 = (lo > -kInfty ? 1 : 0) | (hi < kInfty ? 2 : 0);
+                act2 |= st0 & ~stb & 3;
+            }
+            if (status != ST_OK) act2 = 0;
+        }
     }
 
 #undef MPCQP_BLO
@@ -1500,6 +1542,25 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         const int b0 = __builtin_amdgcn_readlane(bo, 0), b1 = __builtin_amdgcn_readlane(bo, kHalf);
         const uint64_t dm = __ballot(defer && bo >= 0);
         if (dm && lno == 0) wg_list_append(a.ovf, a.ovf_cap, b0, dm & 1ull, b1, (dm >> kHalf) & 1ull);
+    }
+    if constexpr (GEN) {
+        // warm start: this tick's active bounds, in the global numbering (bit v lower, bit NV + v
+        // upper: gi_reg.hpp WarmSet), for the next tick -- every instance of the launch writes
+        // its words (zero when it was not solved)
+        if (a.warm) {
+            unsigned long long *wl = reinterpret_cast<unsigned long long *>(Do + Lay::oRow);
+            wave_sync();
+            if (hlo < a.warm_words) wl[hlo] = 0ull;
+            wave_sync();
+            if (bo >= 0 && hlo < nf && nf <= NF && act2) {
+                const int v = fido[hlo];
+                if (act2 & 1) atomicOr(&wl[v >> 6], 1ull << (v & 63));
+                if (act2 & 2) atomicOr(&wl[(NV + v) >> 6], 1ull << ((NV + v) & 63));
+            }
+            wave_sync();
+            if (bo >= 0 && hlo < a.warm_words) a.warm[(size_t)bo * a.warm_words + hlo] = wl[hlo];
+            wave_sync();
+        }
     }
     if (bo >= 0 && !defer) {
         // U assembled in LDS (the dead L / R space), then written once, coalesced: a

@@ -1633,7 +1633,7 @@ int mpcqp_ctx_reserve(mpcqp_ctx *c, int B) {
     if (!rc && c->fast && c->fk.wg) rc = ensure_list(c, B);
     if (!rc && c->fast && c->fk.mpc_gen)
         rc = ensure_bytes(c, &c->rbuf, &c->rbuf_cap, rollout_bytes(c, B, 1));
-    if (!rc && c->warm_on && c->fast && c->fk.mpc_gen && !c->fk.pair_gen) rc = ensure_warm(c, B);
+    if (!rc && c->warm_on && c->fast && c->fk.mpc_gen) rc = ensure_warm(c, B);
     if (!rc && !c->fast) rc = ensure_bytes(c, (void **)&c->dAB, &c->ab_cap, sizeof(double) * ab * B);
     if (!rc && !c->fast) rc = ensure_scratch_hf(c, B);
     if (!rc) rc = hip_status(hipStreamSynchronize(c->stream));
@@ -1957,7 +1957,7 @@ int mpcqp_batch_solve_gait(mpcqp_ctx *c, int S, int C, const double *state, cons
     a.cost = cost;
     a.status = status;
     a.iters = iters;
-    if (c->warm_on && !c->fk.pair_gen) {  // the one-wave kernels (N = 20 / literal) take it
+    if (c->warm_on) {  // the paired kernel seeds its crash start, the one-wave kernels their dual loop
         const int rw = ensure_warm(c, B);
         if (rw) return rw;
         a.warm = reinterpret_cast<unsigned long long *>(c->dwarm);
