@@ -12,7 +12,8 @@
 // step s (k = (l >> 4) + 4 s, column l & 15) of S, and the A operand of step s of S' -- every
 // operand below is one conflict-free ds_read_b64 at the same offset:
 //   H / L tiles (i > j) store their TRANSPOSE (S = L_ij'),  X tiles store X_ij itself,
-//   the diagonal tile k ends up holding W_k = L_kk^-1 (= X_kk), Wt[k] holds W_k'.
+//   the diagonal tile k ends up holding W_k = L_kk^-1 (= X_kk), Wt[k] holds W_k' (padded
+//   layout, see diag_block_inverse_l).
 // Algorithm (T = NF / 16 block columns):
 //   for k:  W_k = (chol of tile k)^-1 on wave 0 (16 lanes, registers)        | barrier
 //           L_ik' = W_k H_ik'                (A = W_k, B = H_ik', 4 MFMAs)    | barrier
@@ -30,6 +31,7 @@ struct TileFact {
     static_assert(NF % 16 == 0, "16-column blocks");
     static constexpr int T = NF / 16;
     static constexpr int TS = 272;  // 256 + 16: tiles (i, j) and (i, j + 1) sit 16 bank pairs apart
+                                    // (and a W' slot holds the padded (68, 17) layout: 271)
     static constexpr int NT = T * (T + 1) / 2;
     static constexpr int oTiles = 0;
     static constexpr int oWt = NT * TS;        // W_k' slices
@@ -98,15 +100,27 @@ __device__ __forceinline__ void diag_factor_dpp(double (&a)[16], double (&w)[16]
         diag_factor_dpp<K + 1>(a, w, bad);
     }
 }
-__device__ __forceinline__ void diag_block_inverse_rl(double *tile, double *wt, bool &bad);
-__device__ __forceinline__ void diag_block_inverse(double *tile, double *wt, bool &bad) {
+// Layouts: element (a, b) of a 16 x 16 tile at P4 (a >> 2) + P1 (a & 3) + b.  (64, 16) is the
+// MFMA slice order (register s of lane l at 64 s + l); there the row reads below (lane i reads
+// row i) stride 16 doubles and land on two bank pairs: 8-way conflicts, and so do the row
+// stores of W'.  (68, 17) pads each 16-double group by one and each slice by four: the 16 rows
+// start on distinct bank pairs, and slice reads (68 s + 17 (l >> 4) + (l & 15)) stay
+// conflict-free but for one lane pair.  diag_block_inverse_l reads the block from src in
+// (S4, S1), writes W to wd in (W4, W1) and W' to td in (T4, T1); src may alias either output
+// (every read precedes every write).
+template <int S4, int S1, int W4, int W1, int T4, int T1>
+__device__ __forceinline__ void diag_block_inverse_rl(const double *src, double *wd, double *td,
+                                                      bool &bad);
+template <int S4, int S1, int W4, int W1, int T4, int T1>
+__device__ __forceinline__ void diag_block_inverse_l(const double *src, double *wd, double *td,
+                                                     bool &bad) {
 #if MPCQP_DIAG_DPP
     const int ln = lane();
     const int li = ln & 15;
     double a[16], w[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-        a[j] = (j <= li) ? tile[64 * (li >> 2) + 16 * (li & 3) + j] : 0.0;
+        a[j] = (j <= li) ? src[S4 * (li >> 2) + S1 * (li & 3) + j] : 0.0;
         w[j] = (li == j) ? 1.0 : 0.0;
     }
     // (every row computes the same pivots; the ballot keeps the flag wave-uniform for the
@@ -117,22 +131,28 @@ __device__ __forceinline__ void diag_block_inverse(double *tile, double *wt, boo
     if (ln < 16) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            tile[64 * (i >> 2) + 16 * (i & 3) + li] = w[i];   // W(i, c), c = li
-            wt[64 * (li >> 2) + 16 * (li & 3) + i] = w[i];    // W'(c, i)
+            wd[W4 * (i >> 2) + W1 * (i & 3) + li] = w[i];   // W(i, c), c = li
+            td[T4 * (li >> 2) + T1 * (li & 3) + i] = w[i];  // W'(c, i)
         }
     }
     return;
 #endif
-    diag_block_inverse_rl(tile, wt, bad);
+    diag_block_inverse_rl<S4, S1, W4, W1, T4, T1>(src, wd, td, bad);
 }
-__device__ __forceinline__ void diag_block_inverse_rl(double *tile, double *wt, bool &bad) {
+// the block in place in the slice order, W' to wt in the slice order
+__device__ __forceinline__ void diag_block_inverse(double *tile, double *wt, bool &bad) {
+    diag_block_inverse_l<64, 16, 64, 16, 64, 16>(tile, tile, wt, bad);
+}
+template <int S4, int S1, int W4, int W1, int T4, int T1>
+__device__ __forceinline__ void diag_block_inverse_rl(const double *src, double *wd, double *td,
+                                                      bool &bad) {
     const int ln = lane();
     const bool on = ln < 16;
     const int li = ln & 15;
     double a[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j)
-        a[j] = (on && j <= li) ? tile[64 * (li >> 2) + 16 * (li & 3) + j] : 0.0;
+        a[j] = (on && j <= li) ? src[S4 * (li >> 2) + S1 * (li & 3) + j] : 0.0;
     double iq[16];
     double w[16];  // lane c: column c of W = L^-1 (fused form: e_c, reduced step by step)
 #pragma unroll
@@ -169,8 +189,8 @@ __device__ __forceinline__ void diag_block_inverse_rl(double *tile, double *wt, 
     if (on) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            tile[64 * (i >> 2) + 16 * (i & 3) + li] = w[i];   // W(i, c), c = li
-            wt[64 * (li >> 2) + 16 * (li & 3) + i] = w[i];    // W'(c, i)
+            wd[W4 * (i >> 2) + W1 * (i & 3) + li] = w[i];   // W(i, c), c = li
+            td[T4 * (li >> 2) + T1 * (li & 3) + i] = w[i];  // W'(c, i)
         }
     }
 }
@@ -185,6 +205,9 @@ __device__ __forceinline__ void diag_block_inverse_rl(double *tile, double *wt, 
 #ifndef MPCQP_CHOL_LOOKAHEAD
 #define MPCQP_CHOL_LOOKAHEAD 1
 #endif
+#ifndef MPCQP_WG_DIAG_PAD
+#define MPCQP_WG_DIAG_PAD 1
+#endif
 template <int NF, int NW>
 __device__ __forceinline__ bool chol_inverse_mfma(double *F, int wv) {
     using TF = TileFact<NF>;
@@ -193,8 +216,25 @@ __device__ __forceinline__ bool chol_inverse_mfma(double *F, int wv) {
     const int ln = lane();
     double *tiles = F + TF::oTiles, *Wt = F + TF::oWt;
     bool bad = false;
+    // MPCQP_WG_DIAG_PAD: the diagonal block is staged into W_k''s slot in the padded (68, 17)
+    // layout, factored from there (conflict-free row reads), W_k lands in the tile in slice order
+    // and W_k' in the padded layout (conflict-free row stores), which the panel and X products
+    // read as slices (68 s + so).  0: everything in slice order (A/B builds).
+    constexpr int Q4 = MPCQP_WG_DIAG_PAD ? 68 : 64, Q1 = MPCQP_WG_DIAG_PAD ? 17 : 16;
+    const int so = Q1 * (ln >> 4) + (ln & 15);
     auto diag = [&](int k) {
-        diag_block_inverse(tiles + TS * tix(k, k), Wt + TS * k, bad);
+        double *tk = tiles + TS * tix(k, k), *wk = Wt + TS * k;
+        if constexpr (MPCQP_WG_DIAG_PAD) {
+            double v[4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) v[s] = tk[64 * s + ln];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) wk[Q4 * s + so] = v[s];
+            wave_sync();
+            diag_block_inverse_l<Q4, Q1, 64, 16, Q4, Q1>(wk, tk, wk, bad);
+        } else {
+            diag_block_inverse(tk, wk, bad);
+        }
         if (ln == 0 && bad) F[TF::oFlag] = 1.0;
     };
     // trailing pair t of step k (k < j <= i, row-major: t = 0 is the diagonal tile (k+1, k+1))
@@ -227,7 +267,7 @@ __device__ __forceinline__ bool chol_inverse_mfma(double *F, int wv) {
             dx4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int s = 0; s < 4; ++s)
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(wk[64 * s + ln], ti[64 * s + ln], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(wk[Q4 * s + so], ti[64 * s + ln], acc, 0, 0, 0);
 #pragma unroll
             for (int s = 0; s < 4; ++s) ti[64 * s + ln] = acc[s];
         }
@@ -268,7 +308,7 @@ __device__ __forceinline__ bool chol_inverse_mfma(double *F, int wv) {
             dx4 x = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int s = 0; s < 4; ++s)
-                x = __builtin_amdgcn_mfma_f64_16x16x4f64(-wi[64 * s + ln], q[s], x, 0, 0, 0);
+                x = __builtin_amdgcn_mfma_f64_16x16x4f64(-wi[Q4 * s + so], q[s], x, 0, 0, 0);
             xr[u] = x;
         }
         __syncthreads();  // every read of L_i* is done before X_i* overwrites it

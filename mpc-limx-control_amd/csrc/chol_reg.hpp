@@ -7,10 +7,17 @@
 // operand of step s of S and the A operand of step s of S'):
 //   off-diagonal L tiles hold L_ij', X tiles hold X_ij, the diagonal tile holds H_kk (lower
 //   triangle valid) until its block is factored, then W_k = L_kk^-1; wt[k] holds W_k'.
-// LDS: 576 doubles of scratch (diagonal-block staging, X-tile readout, g), over the packed H
-// once every tile is loaded.
+// LDS: 608 doubles of scratch (diagonal-block staging and X-tile readout in the padded layout
+// (68, 17) of diag_block_inverse_l, W' staging, g), over the packed H once every tile is loaded.
+// (The (64, 16) slice order made every row read of the staged tile an 8-way bank conflict: the
+// diagonal factorisation's loads and W' stores and the t = X g readout.)
 #pragma once
 #include "chol_mfma.hpp"
+
+// MPCQP_CHOL_PAD: stage tiles in the padded (68, 17) layout; 0: the (64, 16) slice order (A/B)
+#ifndef MPCQP_CHOL_PAD
+#define MPCQP_CHOL_PAD 1
+#endif
 
 namespace mpcqp {
 
@@ -22,7 +29,9 @@ __device__ __forceinline__ void reg_chol_inverse_mfma(const double *Hb, int nf, 
                                                       double &t, bool &bad) {
     constexpr int T = (NF + 15) / 16, NT = T * (T + 1) / 2;
     const int ln = lane(), li = ln & 15, lk = ln >> 4;
-    double *gbuf = scratch + 512;
+    constexpr int P4 = MPCQP_CHOL_PAD ? 68 : 64, P1 = MPCQP_CHOL_PAD ? 17 : 16, PS = 272;  // padded tile layout and its footprint
+    double *gbuf = scratch + 2 * PS;
+    const int so = P1 * lk + li;               // this lane's slot of slice s: P4 s + so
     dx4 tl[NT];
     dx4 wt[T];
     // ---- tiles from the packed H (symmetric reads; identity padding)
@@ -45,14 +54,14 @@ __device__ __forceinline__ void reg_chol_inverse_mfma(const double *Hb, int nf, 
 #pragma unroll
     for (int k = 0; k < T; ++k) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) scratch[64 * s + ln] = tl[tix(k, k)][s];
+        for (int s = 0; s < 4; ++s) scratch[P4 * s + so] = tl[tix(k, k)][s];
         wave_sync();
-        diag_block_inverse(scratch, scratch + 256, bad);
+        diag_block_inverse_l<P4, P1, P4, P1, P4, P1>(scratch, scratch, scratch + PS, bad);
         wave_sync();
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            tl[tix(k, k)][s] = scratch[64 * s + ln];
-            wt[k][s] = scratch[256 + 64 * s + ln];
+            tl[tix(k, k)][s] = scratch[P4 * s + so];
+            wt[k][s] = scratch[PS + P4 * s + so];
         }
         wave_sync();
 #pragma unroll
@@ -107,19 +116,19 @@ __device__ __forceinline__ void reg_chol_inverse_mfma(const double *Hb, int nf, 
 #pragma unroll
         for (int j = 0; j <= i; ++j) {
 #pragma unroll
-            for (int s = 0; s < 4; ++s) scratch[64 * s + ln] = tl[tix(i, j)][s];
+            for (int s = 0; s < 4; ++s) scratch[P4 * s + so] = tl[tix(i, j)][s];
             wave_sync();
             if (lk == j) {
 #pragma unroll
                 for (int cc = 0; cc < 16; ++cc)
                     if (16 * i + cc < NF)
                         Jr[16 * i + cc < NF ? 16 * i + cc : 0] =
-                            scratch[64 * (cc >> 2) + 16 * (cc & 3) + li];
+                            scratch[P4 * (cc >> 2) + P1 * (cc & 3) + li];
             }
             if (lk == i) {
 #pragma unroll
                 for (int cc = 0; cc < 16; ++cc)
-                    tt += scratch[64 * (li >> 2) + 16 * (li & 3) + cc] * gbuf[16 * j + cc];
+                    tt += scratch[P4 * (li >> 2) + P1 * (li & 3) + cc] * gbuf[16 * j + cc];
             }
             wave_sync();
         }

@@ -151,6 +151,7 @@ __device__ __forceinline__ void gi_run_reg(GiCtx &C, double (&h)[NF], double g, 
         if (status == ST_OK && nf > 0) {
             bool bad = false;
             double tt = 0.0;
+            static_assert(RegPack<NF>::doubles >= 608, "chol_reg.hpp scratch fits the R space");
             reg_chol_inverse_mfma<NF>(L.R, nf, g, L.R, Jr, tt, bad);
             if (bad) status = ST_NOT_PD;
             gv = (ln < NF) ? tt : 0.0;

@@ -399,7 +399,19 @@ __device__ __forceinline__ void gi_run_wg(GiCtx &C, double (&hr)[NF / 2], double
         }
         double tt = 0.0;
         if (live) {
-            for (int c = 0; c <= r; ++c) tt += F[TF::xoff(r, c)] * F[TF::oG + c];
+            // t_r = sum_c X(r, c) g_c, block by block; lane r starts block cb at column
+            // (r & 15): row reads of a slice-order tile stride 16 doubles across the lanes (8-way
+            // bank conflicts in column order), rotated they hit 16 distinct bank pairs.  The
+            // diagonal tile's entries above the diagonal are exact zeros.
+            const double *xr = F + TF::oTiles + TS * tix(r >> 4, 0) + 16 * (r & 15);
+            for (int cb = 0; cb <= (r >> 4); ++cb) {
+                const double *gb = F + TF::oG + 16 * cb;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const int cc = (k + r) & 15;
+                    tt += xr[TS * cb + cc] * gb[cc];
+                }
+            }
         }
         gv = (live && r < nf) ? tt : 0.0;
         __syncthreads();  // the factorisation's tiles are dead: the loop's buffers overlay them
