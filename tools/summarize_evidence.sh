@@ -6,7 +6,7 @@ set -e
 T=$1; O=gpurun_out/ev_$T
 # the library the GPU run profiled (its bench line), not whatever is built in-tree now
 export MPCQP_PROFILED_BUILD_ID=$(python3 -c "import json,sys; print(json.load(open(sys.argv[1]))['roofline']['lib_build_id'])" $O/bench.json)
-KB='k_mpc_pair<6, 10, 0, false>'; KC='k_mpc<6, 20, 0, true, 60>'; KE='k_dense_wg<24, 6, 16, true>'
+KB='k_mpc_pair<6, 10, 0, false, 4>'; KC='k_mpc<6, 20, 0, true, 60>'; KE='k_dense_wg<24, 6, 16, true>'
 python3 tools/summarize_profile.py $O/B $T --kernel "$KB" --grid 2097152
 python3 tools/summarize_flops.py $O/B_flops $T --kernel "$KB" --grid 2097152
 python3 tools/summarize_profile.py $O/C ${T}_C --config C --batch 65536 --kernel "$KC" --grid 4194304 --no-traffic-json

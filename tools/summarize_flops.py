@@ -27,7 +27,7 @@ def kernel_tag(name):
 
 def per_dispatch(path, kernel, grid=None):
     """{counter: median over dispatches of `kernel` (exact instantiation when it names one,
-    e.g. 'k_mpc_pair<6, 10, 0, false>', else a substring) at `grid` threads of the
+    e.g. 'k_mpc_pair<6, 10, 0, false, 4>', else a substring) at `grid` threads of the
     per-dispatch total}"""
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(path)):

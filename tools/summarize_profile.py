@@ -20,7 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def kernel_tag(name):
-    """'k_mpc_pair<6, 10, 0, false>' out of the demangled signature."""
+    """'k_mpc_pair<6, 10, 0, false, 4>' out of the demangled signature."""
     i = name.find("k_")
     j = name.find(">", i)
     return name[i:j + 1] if i >= 0 and j > i else name
@@ -77,7 +77,7 @@ def main():
     ap.add_argument("tag")
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--config", default="B")
-    ap.add_argument("--kernel", default="k_mpc_pair<6, 10, 0, false>")
+    ap.add_argument("--kernel", default="k_mpc_pair<6, 10, 0, false, 4>")
     ap.add_argument("--grid", type=int, default=None,
                     help="threads per launch (default: 32 x batch, the pair kernel's grid)")
     ap.add_argument("--no-traffic-json", action="store_true",

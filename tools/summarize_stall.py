@@ -2,7 +2,7 @@
 """Per-launch SQ stall / issue counters of one kernel instantiation and grid (tools/pmc_stall.sh
 output) -> profiles/<tag>_stall.json.  SQ_*_CYCLES-type counters are in quad-cycles summed over
 waves; fractions are taken against SQ_WAVE_CYCLES.
-Usage: tools/summarize_stall.py DIR TAG [--kernel 'k_mpc_pair<6, 10, 0, false>'] [--grid 2097152]"""
+Usage: tools/summarize_stall.py DIR TAG [--kernel 'k_mpc_pair<6, 10, 0, false, 4>'] [--grid 2097152]"""
 import argparse
 import collections
 import csv
@@ -25,7 +25,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("tag")
-    ap.add_argument("--kernel", default="k_mpc_pair<6, 10, 0, false>")
+    ap.add_argument("--kernel", default="k_mpc_pair<6, 10, 0, false, 4>")
     ap.add_argument("--grid", type=int, default=2097152)
     a = ap.parse_args()
     vals = collections.defaultdict(list)
