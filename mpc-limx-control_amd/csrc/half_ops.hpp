@@ -24,12 +24,67 @@ __device__ __forceinline__ double ll2d(int lo, int hi) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-// (even row, odd row) of this half for a row-uniform value
-__device__ __forceinline__ void row_pair(double v, double &even, double &odd) {
+// Lane masks known at compile time: selects by an SGPR constant (s_mov_b64, scalar) instead of
+// a per-lane v_cmp of the lane index on the VALU.  hmask<K>: lane K of each half.
+template <int K>
+__device__ __forceinline__ constexpr unsigned long long hmask() {
+    return (1ull << K) | (1ull << (K + kHalf));
+}
+// lanes lo..hi (inclusive) of each half
+template <int LO, int HI>
+__device__ __forceinline__ constexpr unsigned long long hrange() {
+    constexpr unsigned long long h = LO > HI ? 0ull : ((~0ull >> (63 - HI)) & ~((1ull << LO) - 1ull));
+    return h | (h << kHalf);
+}
+// the same for indices that are constants after unrolling (the shifts fold)
+__device__ __forceinline__ unsigned long long hmask_k(int k) {
+    return (1ull << k) | (1ull << (k + kHalf));
+}
+__device__ __forceinline__ unsigned long long hrange_k(int lo, int hi) {
+    const unsigned long long h = lo > hi ? 0ull : ((~0ull >> (63 - hi)) & ~((1ull << lo) - 1ull));
+    return h | (h << kHalf);
+}
+// m ? 0.0 : v, lane by lane
+__device__ __forceinline__ double zero_if(double v, unsigned long long m) {
     const long long b = d2ll(v);
     const int lo = (int)(b & 0xffffffffll), hi = (int)(b >> 32);
-    const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-    const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    int rl, rh;  // (separate outputs: the input stays where it is, no copy)
+    asm("v_cndmask_b32_e64 %0, %1, 0, %2" : "=v"(rl) : "v"(lo), "s"(m));
+    asm("v_cndmask_b32_e64 %0, %1, 0, %2" : "=v"(rh) : "v"(hi), "s"(m));
+    return ll2d(rl, rh);
+}
+// m ? -v : v, lane by lane (the sign bit of the high word flipped by the select's own source
+// modifier: one instruction)
+__device__ __forceinline__ double neg_if(double v, unsigned long long m) {
+    const long long b = d2ll(v);
+    const int lo = (int)(b & 0xffffffffll), hi = (int)(b >> 32);
+    int rh;
+    asm("v_cndmask_b32_e64 %0, %1, -%1, %2" : "=v"(rh) : "v"(hi), "s"(m));
+    return ll2d(lo, rh);
+}
+
+// one v_mov_b64 (the compiler copies a double it must keep as two v_mov_b32)
+__device__ __forceinline__ double copy64(double v) {
+    double r;
+    asm("v_mov_b64 %0, %1" : "=v"(r) : "v"(v));
+    return r;
+}
+// (even row, odd row) of this half for a row-uniform value.  The swap overwrites both of its
+// operands, so v (still live) is copied twice, 64 bits at a time.
+__device__ __forceinline__ void row_pair(double v, double &even, double &odd) {
+    const long long b1 = d2ll(copy64(v)), b2 = d2ll(copy64(v));
+    const auto l = __builtin_amdgcn_permlane16_swap((int)(b1 & 0xffffffffll), (int)(b2 & 0xffffffffll),
+                                                     false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap((int)(b1 >> 32), (int)(b2 >> 32), false, false);
+    even = ll2d(l[0], h[0]);
+    odd = ll2d(l[1], h[1]);
+}
+// the same for a value that dies here: one copy, the swap takes v's own registers
+__device__ __forceinline__ void row_pair_dead(double v, double &even, double &odd) {
+    const long long b1 = d2ll(copy64(v)), b2 = d2ll(v);
+    const auto l = __builtin_amdgcn_permlane16_swap((int)(b1 & 0xffffffffll), (int)(b2 & 0xffffffffll),
+                                                     false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap((int)(b1 >> 32), (int)(b2 >> 32), false, false);
     even = ll2d(l[0], h[0]);
     odd = ll2d(l[1], h[1]);
 }
@@ -45,7 +100,7 @@ __device__ __forceinline__ double hbcast(double v) {
     static_assert(K >= 0 && K < kHalf, "lane within a half");
     const double r = dpp<0x150 + (K & 15)>(v);  // row_newbcast
     double e, o;
-    row_pair(r, e, o);
+    row_pair_dead(r, e, o);
     return K < 16 ? e : o;
 }
 // the same for an index that is constant after unrolling (the switch folds)

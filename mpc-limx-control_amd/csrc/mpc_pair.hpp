@@ -241,12 +241,12 @@ __device__ __forceinline__ int pair_sorted_instance(const MpcArgs &a) {
 // row_pair), times the lane's own multiplier m.  Columns k (A0/B0, m0) and k + 1 (A1/B1, m1).
 // The compiler does not form DPP FMAs itself (its VOP3 v_fma_f64 has no DPP); "s_nop 1" gives
 // the DPP source its two wait states after the VALU that wrote it.
-template <int J>
+template <int J, bool NOP>
 __device__ __forceinline__ void fold_dpp4(double &s0, double &s1, double &s2, double &s3,
                                           double A0, double B0, double m0, double A1, double B1,
                                           double m1) {
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, -%4, %12 row_newbcast:%c14 row_mask:0xf bank_mask:0xf\n\t"
+    if constexpr (NOP) asm volatile("s_nop 1");
+    asm("v_fmac_f64_dpp %0, -%4, %12 row_newbcast:%c14 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, -%5, %12 row_newbcast:%c15 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %2, -%6, %12 row_newbcast:%c16 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %3, -%7, %12 row_newbcast:%c17 row_mask:0xf bank_mask:0xf\n\t"
@@ -260,11 +260,11 @@ __device__ __forceinline__ void fold_dpp4(double &s0, double &s1, double &s2, do
           "v"(J + 2 < 16 ? A1 : B1), "v"(J + 3 < 16 ? A1 : B1), "v"(m0), "v"(m1),
           "i"(J & 15), "i"((J + 1) & 15), "i"((J + 2) & 15), "i"((J + 3) & 15));
 }
-template <int J>
+template <int J, bool NOP>
 __device__ __forceinline__ void fold_dpp2(double &s0, double &s1, double A0, double B0, double m0,
                                           double A1, double B1, double m1) {
-    asm("s_nop 1\n\t"
-        "v_fmac_f64_dpp %0, -%2, %6 row_newbcast:%c8 row_mask:0xf bank_mask:0xf\n\t"
+    if constexpr (NOP) asm volatile("s_nop 1");
+    asm("v_fmac_f64_dpp %0, -%2, %6 row_newbcast:%c8 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, -%3, %6 row_newbcast:%c9 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %0, -%4, %7 row_newbcast:%c8 row_mask:0xf bank_mask:0xf\n\t"
         "v_fmac_f64_dpp %1, -%5, %7 row_newbcast:%c9 row_mask:0xf bank_mask:0xf"
@@ -284,11 +284,13 @@ __device__ __forceinline__ void fold_dpp1(double &s, double A, double B, double 
 template <int NF, int K, int J = K + 2>
 __device__ __forceinline__ void fold_trailing(double (&s)[NF], double A0, double B0, double m0,
                                               double A1, double B1, double m1) {
+    // (the DPP sources A / B were written before the step's first group: only that group
+    //  needs the two wait states after the VALU that wrote them)
     if constexpr (J + 3 < NF) {
-        fold_dpp4<J>(s[J], s[J + 1], s[J + 2], s[J + 3], A0, B0, m0, A1, B1, m1);
+        fold_dpp4<J, J == K + 2>(s[J], s[J + 1], s[J + 2], s[J + 3], A0, B0, m0, A1, B1, m1);
         fold_trailing<NF, K, J + 4>(s, A0, B0, m0, A1, B1, m1);
     } else if constexpr (J + 1 < NF) {
-        fold_dpp2<J>(s[J], s[J + 1], A0, B0, m0, A1, B1, m1);
+        fold_dpp2<J, J == K + 2>(s[J], s[J + 1], A0, B0, m0, A1, B1, m1);
         fold_trailing<NF, K, J + 2>(s, A0, B0, m0, A1, B1, m1);
     }
 }
@@ -771,27 +773,29 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
             static_assert(MPCQP_CHOL_CB == 2, "the folded sweep runs column pairs");
             double *dg = rot;  // pivot of every column (uniform stores), for the final scaling
             double piv = hbcast<0>(Jr[0]);
-            int bad = !(piv > 0.0);  // (an int pinned every step: see below)
+            // non-PD flag: a lane mask in SGPRs (v_cmp + s_or per pivot), pinned every step
+            unsigned long long badm = __ballot(!(piv > 0.0));
             double ik = rsqrt_nr(piv);
     #pragma unroll
             for (int k = 0; k < NF; k += 2) {
                 const double pk = piv;
                 // column k: lanes > k get L(l, k), lanes < k their J entry y_k; lane k L(k, k),
                 // negated (its J part's first entry), and multiplier 0 (it sits out step k)
+                // (lane k of each half by an SGPR constant: no per-lane compare)
                 Jr[k] *= ik;
-                const bool own0 = hl == k;
-                const double m0 = own0 ? 0.0 : Jr[k];
-                Jr[k] = own0 ? -Jr[k] : Jr[k];
+                const unsigned long long own0 = hmask_k(k);
+                const double m0 = zero_if(Jr[k], own0);
+                Jr[k] = neg_if(Jr[k], own0);
                 double A0, B0;
                 row_pair(m0, A0, B0);  // the column's rows 0-15 / 16-31 in every row of the half
                 fold_in_panel<NF>(Jr, A0, B0, m0, k);  // slot k + 1 -= L(k + 1, k) m0
                 const double pc = hbcast(Jr[k + 1], k + 1);
-                bad |= !(pc > 0.0) ? 1 : 0;
+                badm |= __ballot(!(pc > 0.0));
                 const double ik1 = rsqrt_nr(pc);
                 Jr[k + 1] *= ik1;
-                const bool own1 = hl == k + 1;
-                const double m1 = own1 ? 0.0 : Jr[k + 1];
-                Jr[k + 1] = own1 ? -Jr[k + 1] : Jr[k + 1];
+                const unsigned long long own1 = hmask_k(k + 1);
+                const double m1 = zero_if(Jr[k + 1], own1);
+                Jr[k + 1] = neg_if(Jr[k + 1], own1);
                 double A1, B1;
                 row_pair(m1, A1, B1);
                 double pivn = 1.0, ikn = 1.0;
@@ -799,7 +803,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                     double hn = Jr[k + 2 < NF ? k + 2 : k];
                     hn -= Jr[k] * Jr[k];
                     pivn = hbcast(hn - Jr[k + 1] * Jr[k + 1], k + 2);
-                    bad |= !(pivn > 0.0) ? 1 : 0;
+                    badm |= __ballot(!(pivn > 0.0));
                     ikn = rsqrt_nr(pivn);
                 }
                 dg[k] = pk;
@@ -816,7 +820,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 pin(ik);
                 // the non-PD test is evaluated here, each step: left to the compiler, every
                 // column's pivot stayed live to a test sunk after the sweep (60 VGPRs)
-                asm volatile("" : "+v"(bad));
+                asm volatile("" : "+s"(badm));
                 step_fence();
             }
             {   // rows of J: slots >= l times -1 / piv_l, the L row below zeroed; lane 31 keeps t
@@ -824,14 +828,17 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                 const bool gl = hl == kHalf - 1;
                 const double pl = dg[hl < NF ? hl : 0];
                 const double cl = gl ? 1.0 : -1.0 / pl;
-                const int lim = gl ? 0 : (hl < NF ? hl : NF);
+                // slot j is zeroed on lanes j + 1 .. NF - 1 (their L rows) and on the padding
+                // lanes NF .. 30 (lane 31 keeps t): a constant lane mask per slot
     #pragma unroll
                 for (int j = 0; j < NF; ++j) {
-                    Jr[j] = (j < lim) ? 0.0 : Jr[j] * cl;
+                    Jr[j] = zero_if(Jr[j] * cl, hrange_k(j + 1, kHalf - 2));
                     pin(Jr[j]);  // (in place: the scaled row does not take a second register set)
                     if ((j & 7) == 7) step_fence();
                 }
             }
+            // (every pivot is uniform over its half: the half's base lane carries its votes)
+            const bool bad = ((badm >> (lane() & kHalf)) & 1ull) != 0ull;
 #else
             // ---- Cholesky fused with the inverse sweep.  Right-looking, lane l owns row l of H_FF
             //      (identity padding beyond nf).  Step k's column of L, broadcast from LDS for the

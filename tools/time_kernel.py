@@ -14,6 +14,9 @@ ap.add_argument("--batch", type=int, default=65536)
 ap.add_argument("--reps", type=int, default=20)
 ap.add_argument("--gait", default="alternating")
 ap.add_argument("--max-free", type=int, default=None)
+ap.add_argument("--b2b", action="store_true",
+                help="launches back to back (no sync between them, as bench.py's steps), the "
+                     "one-wave kernel's mean by the library's events (slot 2) after 50 warm-up calls")
 args = ap.parse_args()
 import mpcqp  # noqa: E402
 from mpcqp.engine import BatchEngine  # noqa: E402
@@ -24,6 +27,20 @@ for cfg in args.configs.split(","):
         p["max_free"] = args.max_free
     eng = BatchEngine(p)
     d = eng.upload(mpcqp.make_batch(p, args.batch, gait=args.gait))
+    if args.b2b:
+        for _ in range(50):
+            eng.solve(d)
+        eng.sync()
+        eng.enable_timing(True)
+        for _ in range(args.reps):
+            eng.solve(d)
+        eng.sync()
+        ms, n = eng.kernel_ms_sum(2)
+        st = d["status"].cpu().numpy()
+        print(f"  {cfg}: {ms / n:.4f} ms  ({args.batch / (ms / n) / 1e3:.2f} M QP/s)  solved "
+              f"{np.mean(st == 0):.4f}  (back to back, {n} launches)")
+        eng.close()
+        continue
     eng.enable_timing(True)
     ts = []
     for r in range(args.reps + 3):
