@@ -64,6 +64,17 @@ constexpr int pair_pf() {
 #endif
 // the folded sweep's rows load from a per-slot selected address (one LDS read per slot) instead
 // of reading both candidates and selecting the value (A/B)
+// MPCQP_FOLD_LMASK: the row load's lower / upper choice (q <= l) by a constant lane mask per
+// slot (no v_cmp of the lane index): fewer VALU, measured neutral (r06p); 0: the compare
+#ifndef MPCQP_FOLD_LMASK
+#define MPCQP_FOLD_LMASK 0
+#endif
+// MPCQP_PAIR_CRASH_RCP: the crash's Gauss-Jordan pivot reciprocal from v_rcp_f64 and two Newton
+// steps (5 VALU instead of the ~12 of the IEEE division; the pivots are positive and normal or
+// the half gives up), and w = r / pivot as r times that reciprocal; 0: IEEE divisions (A/B)
+#ifndef MPCQP_PAIR_CRASH_RCP
+#define MPCQP_PAIR_CRASH_RCP 1
+#endif
 #ifndef MPCQP_FOLD_ASEL
 #define MPCQP_FOLD_ASEL 1
 #endif
@@ -761,7 +772,16 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                              *Hc = D + Lay::oR + hl;
     #pragma unroll
                 for (int q = 0; q < NF; ++q) {
-                    if (MPCQP_FOLD_ASEL) {  // one load from the selected address
+                    if (MPCQP_FOLD_ASEL && MPCQP_FOLD_LMASK) {  // lanes q .. 31 read their row
+                        const unsigned long long mq = hrange_k(q, kHalf - 1);
+                        int ad;
+                        asm("v_cndmask_b32_e64 %0, %1, %2, %3"
+                            : "=v"(ad)
+                            : "v"((int)(size_t)(Hc + lrow(q))), "v"((int)(size_t)(Hr + q)), "s"(mq));
+                        // (the low 32 bits of an LDS-derived generic pointer are its LDS address)
+                        typedef __attribute__((address_space(3))) const double lds_cd;
+                        Jr[q] = *(lds_cd *)(size_t)(unsigned)ad;
+                    } else if (MPCQP_FOLD_ASEL) {  // one load from the selected address
                         Jr[q] = *((q <= hl) ? Hr + q : Hc + lrow(q));  // (q, l) read for q > l
                     } else {
                         const double lo_ = Hr[q], up_ = Hc[lrow(q)];  // (q, l) read for q > l
@@ -1132,8 +1152,17 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                                 }
                             }
                             Pv[KC] = rr;
-                            Pv[KC + 1] = 1.0 / Mr[j];
-                            dd = Mr[j];
+                            if constexpr (MPCQP_PAIR_CRASH_RCP) {
+                                const double pj = Mr[j];
+                                double y = __builtin_amdgcn_rcp(pj);
+                                y = fma(y, fma(-pj, y, 1.0), y);
+                                y = fma(y, fma(-pj, y, 1.0), y);
+                                Pv[KC + 1] = y;
+                                dd = y;  // (its reciprocal: w = r / pivot below)
+                            } else {
+                                Pv[KC + 1] = 1.0 / Mr[j];
+                                dd = Mr[j];
+                            }
                             bad |= !(Mr[j] > 0.0);
                         }
                         wave_sync();
@@ -1159,7 +1188,7 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                     }
                 }
                 const bool gave_up = half_ballot(bad) != 0u;
-                const double w = inA ? rr / dd : 0.0;
+                const double w = inA ? (MPCQP_PAIR_CRASH_RCP ? rr * dd : rr / dd) : 0.0;
                 if (inA) Wv[rho] = w;
                 // (b and the right-hand side re-derived after the elimination: not live through it)
                 const double bval = side > 0 ? MPCQP_BLO : -MPCQP_BHI;
