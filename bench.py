@@ -245,13 +245,17 @@ def host_staged_rate(eng, batch, p, reps=5, locked=False):
     import ctypes as C
 
     from mpcqp._lib import lib
+    from mpcqp import page_aligned, page_aligned_empty
     B = batch["x0"].shape[0]
     nV = p["nu"] * p["N"]
-    U = np.zeros(B * nV)
-    cost = np.zeros(B)
-    st = np.zeros(B, np.int32)
-    it = np.zeros(B, np.int32)
-    ins = [np.ascontiguousarray(batch[k]) for k in ("x0", "xref", "lin", "contact")]
+    # registered buffers start on a page and own their pages (include/mpcqp.h)
+    alloc = page_aligned_empty if locked else np.zeros
+    U = alloc(B * nV, np.float64)
+    cost = alloc(B, np.float64)
+    st = alloc(B, np.int32)
+    it = alloc(B, np.int32)
+    ins = [(page_aligned if locked else np.ascontiguousarray)(batch[k])
+           for k in ("x0", "xref", "lin", "contact")]
     ptr = lambda a: C.c_void_p(a.ctypes.data)
     arrs = ins + [U, cost, st, it]
     if locked:

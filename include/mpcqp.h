@@ -233,7 +233,10 @@ int mpcqp_batch_solve_host(mpcqp_ctx *ctx, int B, const double *x0, const double
  * caller's own buffers to the solver; here the device reads them by DMA).  register / unregister
  * wrap an existing allocation (the caller keeps it alive while registered: unregister before
  * freeing it); alloc / free return new page-locked memory.  Registering is expensive (page
- * pinning): do it once per buffer, not per tick. */
+ * pinning): do it once per buffer, not per tick.  register needs a page-aligned p
+ * (MPCQP_ERR_BAD_ARG otherwise) and should cover the buffer's whole pages: pinning works on
+ * pages, and a page shared by two registrations (small heap arrays side by side) leaves the HIP
+ * runtime a stale mapping that can fault a later copy.  mpcqp_host_alloc's memory qualifies. */
 int mpcqp_host_register(void *p, size_t bytes);
 int mpcqp_host_unregister(void *p);
 int mpcqp_host_alloc(size_t bytes, void **p);

@@ -15,6 +15,7 @@
 //   k_select_min per-rank min-cost key (multi-GPU selection)
 //   k_plant      x <- Ad x + Bd u                                       src/QPSolver.cpp:108-111
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <math.h>
 #include <stdio.h>
@@ -1709,6 +1710,12 @@ static void host_graphs_drop(mpcqp_ctx *c) {
 // array is DMA'd straight to and from the device by the host-pointer entry points
 int mpcqp_host_register(void *p, size_t bytes) {
     if (!p || !bytes) return MPCQP_ERR_BAD_ARG;
+    // page-aligned starts only: pinning works on whole pages, and two registrations that share a
+    // page (small heap arrays side by side) left the runtime with a stale mapping of it -- a
+    // later pageable copy through that page faulted the device (r06y).  With aligned starts no
+    // page is ever registered twice.
+    const long page = sysconf(_SC_PAGESIZE);
+    if (page > 0 && ((uintptr_t)p % (uintptr_t)page) != 0) return MPCQP_ERR_BAD_ARG;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MPCQP_ERR_NO_DEVICE;
     return hip_status(hipHostRegister(p, bytes, hipHostRegisterDefault));

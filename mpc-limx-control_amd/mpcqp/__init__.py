@@ -6,6 +6,7 @@ package is the host mirror of the reference's interface for the hot path
 """
 from ._lib import (A_COLMAJOR, A_ROWMAJOR, CONS_BOX, CONS_FRICTION, EXPORTS, LIB_PATH,
                    MODEL_LITERAL, MODEL_SRBM, MPCQP_INFTY, STATUS, MpcqpError, lib)
+from .hostmem import page_aligned, page_aligned_empty
 from .model import model_params, static_foot_offsets
 from .workload import (DEFAULT_SEED, gait_contact_mask, gait_inputs, make_batch,
                        make_gait_states, mpc_test_inputs, qp_harness_inputs)
@@ -14,5 +15,6 @@ __all__ = [
     "A_COLMAJOR", "A_ROWMAJOR", "CONS_BOX", "CONS_FRICTION", "EXPORTS", "LIB_PATH",
     "MODEL_LITERAL", "MODEL_SRBM", "MPCQP_INFTY", "STATUS", "MpcqpError", "lib",
     "model_params", "static_foot_offsets", "DEFAULT_SEED", "gait_contact_mask", "make_batch",
-    "qp_harness_inputs", "mpc_test_inputs", "gait_inputs", "make_gait_states",
+    "qp_harness_inputs", "mpc_test_inputs", "gait_inputs", "make_gait_states", "page_aligned",
+    "page_aligned_empty",
 ]

@@ -72,3 +72,15 @@ def test_model_struct_layout_matches_header(tmp_path):
     M = ml.Model
     assert C.sizeof(M) == size
     assert M.Q.offset == offQ and M.max_free.offset == offmf and M.Ib.offset == offIb
+
+
+def test_host_register_refuses_unaligned_start():
+    """mpcqp_host_register (include/mpcqp.h) takes page-aligned starts only, checked before any
+    device call: two registrations never share a page"""
+    import ctypes as C
+    import numpy as np
+    import mpcqp
+    from mpcqp._lib import lib
+    a = mpcqp.page_aligned(np.arange(1000.0))
+    assert a.ctypes.data % 4096 == 0 and np.array_equal(a, np.arange(1000.0))
+    assert lib().mpcqp_host_register(C.c_void_p(a.ctypes.data + 8), C.c_size_t(64)) == 6

@@ -157,9 +157,12 @@ def test_host_direct_path_equals_device_path(gpu, B, gait):
     eng = BatchEngine(p)
     ref = device_solve(eng, b)
     nV = p["nu"] * p["N"]
-    ins = [np.ascontiguousarray(b[k]) for k in ("x0", "xref", "lin", "contact")]
-    out = dict(U=np.full(B * nV, np.nan), cost=np.full(B, np.nan), status=np.full(B, 99, np.int32),
-               iters=np.full(B, -1, np.int32))
+    # registered buffers start on a page and own their pages (mpcqp_host_register's contract)
+    ins = [mpcqp.page_aligned(b[k]) for k in ("x0", "xref", "lin", "contact")]
+    out = dict(U=mpcqp.page_aligned(np.full(B * nV, np.nan)),
+               cost=mpcqp.page_aligned(np.full(B, np.nan)),
+               status=mpcqp.page_aligned(np.full(B, 99, np.int32)),
+               iters=mpcqp.page_aligned(np.full(B, -1, np.int32)))
     locked = ins + list(out.values())
     _locked(locked, "mpcqp_host_register")
     ptr = lambda a: C.c_void_p(a.ctypes.data)
@@ -174,6 +177,16 @@ def test_host_direct_path_equals_device_path(gpu, B, gait):
     _locked(locked, "mpcqp_host_unregister")
     same(host_solve(eng, p, b), ref)
     eng.close()
+
+
+def test_host_register_needs_page_aligned_start():
+    """mpcqp_host_register refuses a start inside a page (before touching the device): two
+    registrations may never share a page"""
+    from mpcqp._lib import lib
+    import mpcqp
+    a = mpcqp.page_aligned(np.zeros(4096))
+    assert a.ctypes.data % 4096 == 0
+    assert lib().mpcqp_host_register(C.c_void_p(a.ctypes.data + 8), C.c_size_t(64)) == 6
 
 
 def test_host_alloc_roundtrip(gpu):
