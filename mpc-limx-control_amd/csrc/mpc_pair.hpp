@@ -75,6 +75,17 @@ constexpr int pair_pf() {
 #ifndef MPCQP_PAIR_CRASH_RCP
 #define MPCQP_PAIR_CRASH_RCP 1
 #endif
+// MPCQP_PAIR_SLOOP: the S blocks' loop with the lane's entries outermost (see pair_mpc):
+// 260.2 -> 253.4 us at 65,536, 58.7 -> 57.8 us at 8,192 (r06t, profiles/ab_r06t_*)
+#ifndef MPCQP_PAIR_SLOOP
+#define MPCQP_PAIR_SLOOP 1
+#endif
+// MPCQP_CRASH_LSEL: the crash's Gauss-Jordan updates unmasked with a zero multiplier on the
+// lanes that do not eliminate (one select per step instead of one per updated entry): +0.3 % at
+// 65,536 but -0.7 % at 8,192 (r06t), off; 0: the masked update
+#ifndef MPCQP_CRASH_LSEL
+#define MPCQP_CRASH_LSEL 0
+#endif
 #ifndef MPCQP_FOLD_ASEL
 #define MPCQP_FOLD_ASEL 1
 #endif
@@ -549,18 +560,41 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         MPCQP_CUT(a.cut, 13);
 
         // ---- S^W_rr = X_r' W X_r over the support rows (w: 0 = Q, 1 = P), entry o = cj NU + ci
-#pragma unroll
-        for (int blk = 0; blk < 4; ++blk) {
-            const int r_ = blk & 1, w_ = blk >> 1;
-            const int lo = r_ ? Sup::x1lo : Sup::x0lo;
-            const double *Xr = r_ ? X1 : X0;
-            const double *w = w_ ? Pd : Qd;  // diag P / Q (uniform addresses: scalar loads)
+        //      (MPCQP_PAIR_SLOOP: the lane's entries outermost, so their index arithmetic and the
+        //      X rows' loads serve all four blocks; the same operations per entry; 0: the blocks
+        //      outermost, A/B)
+        if constexpr (MPCQP_PAIR_SLOOP) {
             for (int e = hl; e < NRM; e += kHalf) {
                 const int ci = e % NU, cj = e / NU;
-                double acc = 0.0;
+                double acc[4];
 #pragma unroll
-                for (int l = 0; l < SD; ++l) acc += Xr[ci * SD + l] * w[lo + l] * Xr[cj * SD + l];
-                S[e * 4 + blk] = acc;
+                for (int blk = 0; blk < 4; ++blk) {
+                    const int r_ = blk & 1, w_ = blk >> 1;
+                    const int lo = r_ ? Sup::x1lo : Sup::x0lo;
+                    const double *Xr = r_ ? X1 : X0;
+                    const double *w = w_ ? Pd : Qd;  // diag P / Q (uniform addresses: scalar loads)
+                    double a_ = 0.0;
+#pragma unroll
+                    for (int l = 0; l < SD; ++l) a_ += Xr[ci * SD + l] * w[lo + l] * Xr[cj * SD + l];
+                    acc[blk] = a_;
+                }
+#pragma unroll
+                for (int blk = 0; blk < 4; ++blk) S[e * 4 + blk] = acc[blk];
+            }
+        } else {
+#pragma unroll
+            for (int blk = 0; blk < 4; ++blk) {
+                const int r_ = blk & 1, w_ = blk >> 1;
+                const int lo = r_ ? Sup::x1lo : Sup::x0lo;
+                const double *Xr = r_ ? X1 : X0;
+                const double *w = w_ ? Pd : Qd;
+                for (int e = hl; e < NRM; e += kHalf) {
+                    const int ci = e % NU, cj = e / NU;
+                    double acc = 0.0;
+#pragma unroll
+                    for (int l = 0; l < SD; ++l) acc += Xr[ci * SD + l] * w[lo + l] * Xr[cj * SD + l];
+                    S[e * 4 + blk] = acc;
+                }
             }
         }
         // ---- W_m e_m once per (m, support row) -- shared by the NU components -- over the dead
@@ -607,9 +641,10 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
         if (ok && hl < nf) {
             const int vi = fid[hl], ki = vi / NU, ci = vi % NU;
             double s = 0.0;
+            const double kb = (double)ki - 0.5;  // beta = (m - 1) - kb, exact: one conversion per lane
     #pragma unroll
             for (int m = 1; m <= N; ++m) {  // m > ki; unrolled, branch-free: the loads issue together
-                const double beta = (double)(m - 1 - ki) + 0.5;
+                const double beta = (double)(m - 1) - kb;
                 const double tm = UV[(m * 2 + 0) * NU + ci] + beta * UV[(m * 2 + 1) * NU + ci];
                 if (MPCQP_HB_BASES) s = fma((m > ki) ? 1.0 : 0.0, tm, s);  // (exact: x 1 / x 0)
                 else s += (m > ki) ? tm : 0.0;
@@ -1168,7 +1203,9 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                         wave_sync();
                         const double pr = Pv[KC], pi = Pv[KC + 1];
                         const bool upd = inA && rho != j && j < k;
-                        const double l = Mr[j] * pi;
+                        // MPCQP_CRASH_LSEL: the lanes that do not eliminate get multiplier 0 (one
+                        // select) and run the FMAs unmasked: x - 0 * p = x for the finite pivot row
+                        const double l = MPCQP_CRASH_LSEL ? (upd ? Mr[j] * pi : 0.0) : Mr[j] * pi;
                         // the pivot row in chunks of four (loads outside the divergent update,
                         // at most one chunk of it in registers)
         #pragma unroll
@@ -1177,14 +1214,14 @@ __device__ __forceinline__ void pair_mpc(const MpcArgs &a, unsigned char *smem) 
                                 double pv[4];
         #pragma unroll
                                 for (int m = m0; m < m0 + 4; ++m) pv[m - m0] = m > j ? Pv[m] : 0.0;
-                                if (upd) {
+                                if (MPCQP_CRASH_LSEL || upd) {
         #pragma unroll
                                     for (int m = m0; m < m0 + 4; ++m)
                                         if (m > j) Mr[m] -= l * pv[m - m0];
                                 }
                             }
                         }
-                        if (upd) rr -= l * pr;
+                        if (MPCQP_CRASH_LSEL || upd) rr -= l * pr;
                     }
                 }
                 const bool gave_up = half_ballot(bad) != 0u;
