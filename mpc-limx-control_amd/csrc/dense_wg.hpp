@@ -107,6 +107,9 @@ struct DenseLayout {
 #ifndef MPCQP_TOEP_PIPE
 #define MPCQP_TOEP_PIPE 0
 #endif
+#ifndef MPCQP_TOEP_SPLIT
+#define MPCQP_TOEP_SPLIT 1
+#endif
 // The H-row rounds' tile schedule (which wave takes which tile / K half, in the greedy order
 // below) depends only on the shape: computed at compile time, each wave walks its own list
 // (MPCQP_TOEP_SCHED; 0: every wave replays the greedy over all tiles at run time, A/B).  Same
@@ -192,9 +195,27 @@ __device__ __forceinline__ dx4 toep_tile(const double *Ps, const double *Pp, int
         }
         return acc + acc1;
     }
-    for (int mb = mb0; mb < mhi; ++mb) {
+    // MPCQP_TOEP_SPLIT: from the first block where every row of both tiles is live (wave-uniform:
+    // the tiles' last rows' step) the operands load without the zero selects (the same values)
+    const int mfull = MPCQP_TOEP_SPLIT ? max(16 * I + 15 < NV ? (16 * I + 15) / NU : N,
+                                             16 * J + 15 < NV ? (16 * J + 15) / NU : N)
+                                       : N;
+    const int msel = mfull < mhi ? mfull : mhi;
+    for (int mb = mb0; mb < msel; ++mb) {
         double av[KS], bv[KS];
         load(mb, av, bv);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
+    }
+    for (int mb = mb0 > msel ? mb0 : msel; mb < mhi; ++mb) {
+        const double *P = (mb == N - 1 ? Pp : Ps) + mb * NU * LD;
+        const double *pa = P + offa, *pb = P + offb;
+        double av[KS], bv[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            av[s] = pa[4 * s];
+            bv[s] = pb[4 * s];
+        }
 #pragma unroll
         for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
     }
