@@ -347,6 +347,23 @@ int mpcqp_group_sync(mpcqp_group *g) {
     return rc;
 }
 
+// [p, p + bytes) inside page-locked host memory (mpcqp_host_register / mpcqp_host_alloc)?  The
+// same test as the single-context host path's (mpcqp_kernels.hip)
+static bool group_host_locked(const void *p, size_t bytes) {
+    if (!p || !bytes) return false;
+    hipPointerAttribute_t at, at2;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    if (at.type != hipMemoryTypeHost) return false;
+    if (hipPointerGetAttributes(&at2, (const char *)p + bytes - 1) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at2.type == hipMemoryTypeHost;
+}
+
 int mpcqp_group_solve_select_host(mpcqp_group *g, int S, int C, const double *x0,
                                   const double *xref, const double *lin, const uint64_t *contact,
                                   double *U, double *cost, int *status, int *iters,
@@ -372,6 +389,14 @@ int mpcqp_group_solve_select_host(mpcqp_group *g, int S, int C, const double *x0
     std::vector<int *> ps(n), pi(n);
     std::vector<int64_t *> pb(n);
     std::vector<size_t> off_out(n);
+    // the caller's arrays page-locked: each member's shard is DMA'd straight from and into them
+    // (no host memcpy through the staging), as mpcqp_batch_solve_host's direct path
+    const size_t B_all = (size_t)S * C;
+    const bool direct = B_all > 0 && group_host_locked(x0, e_x0 * B_all) &&
+                        group_host_locked(xref, e_xr * B_all) && group_host_locked(lin, e_lin * B_all) &&
+                        (!contact || group_host_locked(contact, e_ct * B_all)) &&
+                        group_host_locked(U, e_u * B_all) && group_host_locked(cost, e_c * B_all) &&
+                        group_host_locked(status, e_s * B_all) && group_host_locked(iters, e_i * B_all);
     for (int i = 0; i < n; ++i) {
         Member &mb = g->mem[i];
         int f = 0, ns = 0;
@@ -405,13 +430,25 @@ int mpcqp_group_solve_select_host(mpcqp_group *g, int S, int C, const double *x0
         }
         const size_t i0 = (size_t)f * C;
         char *h = mb.pin, *d = mb.dbuf;
-        memcpy(h, x0 + i0 * nx, e_x0 * b);
-        memcpy(h + e_x0 * b, xref + i0 * nx * (N + 1), e_xr * b);
-        memcpy(h + (e_x0 + e_xr) * b, lin + i0 * lw, e_lin * b);
-        if (contact) memcpy(h + (e_x0 + e_xr + e_lin) * b, contact + i0, e_ct * b);
-        else memset(h + (e_x0 + e_xr + e_lin) * b, 0, e_ct * b);
-        if (b && hipMemcpyAsync(d, h, e_in * b, hipMemcpyHostToDevice, mb.ss) != hipSuccess)
-            return MPCQP_ERR_DEVICE;
+        if (direct) {
+            const hipMemcpyKind h2d = hipMemcpyHostToDevice;
+            if (b && (hipMemcpyAsync(d, x0 + i0 * nx, e_x0 * b, h2d, mb.ss) != hipSuccess ||
+                      hipMemcpyAsync(d + e_x0 * b, xref + i0 * nx * (N + 1), e_xr * b, h2d,
+                                     mb.ss) != hipSuccess ||
+                      hipMemcpyAsync(d + (e_x0 + e_xr) * b, lin + i0 * lw, e_lin * b, h2d,
+                                     mb.ss) != hipSuccess ||
+                      (contact && hipMemcpyAsync(d + (e_x0 + e_xr + e_lin) * b, contact + i0,
+                                                 e_ct * b, h2d, mb.ss) != hipSuccess)))
+                return MPCQP_ERR_DEVICE;
+        } else {
+            memcpy(h, x0 + i0 * nx, e_x0 * b);
+            memcpy(h + e_x0 * b, xref + i0 * nx * (N + 1), e_xr * b);
+            memcpy(h + (e_x0 + e_xr) * b, lin + i0 * lw, e_lin * b);
+            if (contact) memcpy(h + (e_x0 + e_xr + e_lin) * b, contact + i0, e_ct * b);
+            else memset(h + (e_x0 + e_xr + e_lin) * b, 0, e_ct * b);
+            if (b && hipMemcpyAsync(d, h, e_in * b, hipMemcpyHostToDevice, mb.ss) != hipSuccess)
+                return MPCQP_ERR_DEVICE;
+        }
         px0[i] = (const double *)d;
         pxr[i] = (const double *)(d + e_x0 * b);
         plin[i] = (const double *)(d + (e_x0 + e_xr) * b);
@@ -433,9 +470,21 @@ int mpcqp_group_solve_select_host(mpcqp_group *g, int S, int C, const double *x0
         hipSetDevice(mb.device);
         const size_t b = (size_t)Bm[i], oo = off_out[i];
         const size_t ob = (oo + (e_u + e_c + e_s + e_i) * b + 15) & ~(size_t)15;
-        if (b && hipMemcpyAsync(mb.pin + oo, mb.dbuf + oo, (e_u + e_c + e_s + e_i) * b,
-                                hipMemcpyDeviceToHost, mb.ss) != hipSuccess)
+        if (direct) {
+            const size_t i0 = (size_t)s0[i] * C;
+            const char *d = mb.dbuf + oo;
+            const hipMemcpyKind d2h = hipMemcpyDeviceToHost;
+            if (b && (hipMemcpyAsync(U + i0 * nV, d, e_u * b, d2h, mb.ss) != hipSuccess ||
+                      hipMemcpyAsync(cost + i0, d + e_u * b, e_c * b, d2h, mb.ss) != hipSuccess ||
+                      hipMemcpyAsync(status + i0, d + (e_u + e_c) * b, e_s * b, d2h, mb.ss) !=
+                          hipSuccess ||
+                      hipMemcpyAsync(iters + i0, d + (e_u + e_c + e_s) * b, e_i * b, d2h,
+                                     mb.ss) != hipSuccess))
+                return MPCQP_ERR_DEVICE;
+        } else if (b && hipMemcpyAsync(mb.pin + oo, mb.dbuf + oo, (e_u + e_c + e_s + e_i) * b,
+                                       hipMemcpyDeviceToHost, mb.ss) != hipSuccess) {
             return MPCQP_ERR_DEVICE;
+        }
         if (i == 0 && hipMemcpyAsync(mb.pin + ob, mb.dbuf + ob, rb, hipMemcpyDeviceToHost,
                                      mb.ss) != hipSuccess)
             return MPCQP_ERR_DEVICE;
@@ -446,10 +495,12 @@ int mpcqp_group_solve_select_host(mpcqp_group *g, int S, int C, const double *x0
         const Member &mb = g->mem[i];
         const size_t b = (size_t)Bm[i], oo = off_out[i], i0 = (size_t)s0[i] * C;
         const char *h = mb.pin + oo;
-        memcpy(U + i0 * nV, h, e_u * b);
-        memcpy(cost + i0, h + e_u * b, e_c * b);
-        memcpy(status + i0, h + (e_u + e_c) * b, e_s * b);
-        memcpy(iters + i0, h + (e_u + e_c + e_s) * b, e_i * b);
+        if (!direct) {
+            memcpy(U + i0 * nV, h, e_u * b);
+            memcpy(cost + i0, h + e_u * b, e_c * b);
+            memcpy(status + i0, h + (e_u + e_c) * b, e_s * b);
+            memcpy(iters + i0, h + (e_u + e_c + e_s) * b, e_i * b);
+        }
         if (i == 0) {
             const size_t ob = (oo + (e_u + e_c + e_s + e_i) * b + 15) & ~(size_t)15;
             memcpy(best_host, mb.pin + ob, rb);

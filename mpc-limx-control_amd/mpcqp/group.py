@@ -114,15 +114,18 @@ class Group:
     def sync(self):
         check("mpcqp_group_sync", lib().mpcqp_group_sync(self.g))
 
-    def solve_select_host(self, S: int, Cn: int, batch: dict):
+    def solve_select_host(self, S: int, Cn: int, batch: dict, out: dict | None = None):
         """single-process group: the global host batch of S states x Cn candidates -> dict(U,
-        cost, status, iters, best) (numpy), synchronous"""
+        cost, status, iters, best) (numpy), synchronous.  `out` may hold the U / cost / status /
+        iters arrays to write (e.g. page-locked with mpcqp_host_register, with the batch's input
+        arrays: the library then DMAs straight from and into them)"""
         B = S * Cn
         ins = [np.ascontiguousarray(batch[k]) for k in ("x0", "xref", "lin", "contact")]
-        U = np.zeros((B, self.nV))
-        cost = np.zeros(B)
-        st = np.zeros(B, np.int32)
-        it = np.zeros(B, np.int32)
+        out = out or {}
+        U = out.get("U", np.zeros((B, self.nV)))
+        cost = out.get("cost", np.zeros(B))
+        st = out.get("status", np.zeros(B, np.int32))
+        it = out.get("iters", np.zeros(B, np.int32))
         best = np.zeros(1 + self.nV, np.int64)
         ptr = lambda a: C.c_void_p(a.ctypes.data)
         check("mpcqp_group_solve_select_host",

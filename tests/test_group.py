@@ -114,6 +114,40 @@ def test_group_host_path_matches_solve_select(gpu):
 
 
 @pytest.mark.gpu
+def test_group_host_path_page_locked_matches(gpu):
+    """the group's host path with the caller's arrays page-locked (mpcqp_host_register on
+    page-aligned copies): each member's shard is DMA'd straight from and into them, and every
+    output equals the staged path's bit for bit"""
+    import ctypes as C
+    import mpcqp
+    from mpcqp._lib import lib
+    from mpcqp.group import Group
+    p = mpcqp.model_params("B")
+    S, Cn = 300, 16
+    batch = mpcqp.make_batch(p, S * Cn, seed=5151, gait="mixed")
+    grp = Group(p, devices=[0])
+    ref = grp.solve_select_host(S, Cn, batch)
+    B, nV = S * Cn, p["nu"] * p["N"]
+    locked = {k: mpcqp.page_aligned(batch[k]) for k in ("x0", "xref", "lin", "contact")}
+    out = dict(U=mpcqp.page_aligned(np.full((B, nV), np.nan)),
+               cost=mpcqp.page_aligned(np.full(B, np.nan)),
+               status=mpcqp.page_aligned(np.full(B, 99, np.int32)),
+               iters=mpcqp.page_aligned(np.full(B, -1, np.int32)))
+    arrs = list(locked.values()) + list(out.values())
+    for a in arrs:
+        assert lib().mpcqp_host_register(C.c_void_p(a.ctypes.data), C.c_size_t(a.nbytes)) == 0
+    try:
+        for _ in range(2):
+            got = grp.solve_select_host(S, Cn, locked, out=out)
+            for k in ("U", "cost", "status", "iters", "best"):
+                assert np.array_equal(got[k], ref[k]), k
+    finally:
+        for a in arrs:
+            assert lib().mpcqp_host_unregister(C.c_void_p(a.ctypes.data)) == 0
+    grp.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("gait", ["alternating", "mixed"])
 def test_group_all_devices_matches_whole_batch(gpu, gait):
     """mpcqp_group_create over every visible device (ncclCommInitAll, the grouped all-gather of
