@@ -283,7 +283,11 @@ typedef struct mpcqp_group mpcqp_group;
 /* contiguous shard of whole states for `rank` of `nranks` (host arithmetic, no device): the
  * first `total_states % nranks` ranks take one state more.  bench.py and mpcqp/dist.py use it. */
 int mpcqp_shard(int total_states, int nranks, int rank, int *first_state, int *states);
-/* one process driving `ndev` devices (ncclCommInitAll): ranks 0..ndev-1 = devices[0..ndev-1] */
+/* one process driving `ndev` devices (ncclCommInitAll): ranks 0..ndev-1 = devices[0..ndev-1]
+ * (distinct devices; MPCQP_ERR_BAD_ARG otherwise).  Test transport: with MPCQP_GROUP_LOOPBACK=1
+ * in the environment no communicator is created, the all-gather is device copies between the
+ * members' buffers and members may share a device (the multi-rank orchestration on one GPU;
+ * never for production) */
 int mpcqp_group_create(const mpcqp_model *model, int ndev, const int *devices, mpcqp_group **out);
 /* one process per device (torchrun / MPI style): rank `rank` of `nranks` on `device`.  uid
  * (MPCQP_GROUP_UID_BYTES) comes from mpcqp_group_unique_id on one rank and is handed to every

@@ -64,6 +64,12 @@ struct mpcqp_group {
     int par = 0;
     bool whole = false;   // single process: every rank is a local member
     bool failed = false;  // a step failed part-way: communicators aborted, every call refused
+    // test transport (MPCQP_GROUP_LOOPBACK=1 at mpcqp_group_create): no RCCL communicator; the
+    // all-gather is device copies between the members' buffers, and members may share a device,
+    // so the multi-member orchestration (shards, per-member streams, record double-buffering,
+    // the cross-rank reduction) runs on a one-GPU machine.  Never for production: RCCL is the
+    // transport.
+    bool loopback = false;
     long step = 0;        // steps issued
     long inject = -1;     // fault injection (tests): step MPCQP_GROUP_INJECT_FAIL fails part-way
     std::vector<Member> mem;
@@ -164,12 +170,15 @@ int mpcqp_group_destroy(mpcqp_group *g) {
 int mpcqp_group_create(const mpcqp_model *m, int ndev, const int *devices, mpcqp_group **out) {
     if (!m || !out || ndev <= 0 || !devices) return MPCQP_ERR_BAD_ARG;
     *out = nullptr;
+    const char *lb = getenv("MPCQP_GROUP_LOOPBACK");
+    const bool loopback = lb && atoi(lb) == 1;
     for (int i = 0; i < ndev; ++i)
         for (int j = 0; j < i; ++j)
-            if (devices[i] == devices[j]) return MPCQP_ERR_BAD_ARG;  // one rank per device
+            if (devices[i] == devices[j] && !loopback) return MPCQP_ERR_BAD_ARG;  // one rank per device
     mpcqp_group *g = group_new(m, ndev);
     if (!g) return MPCQP_ERR_DEVICE;
     g->whole = true;
+    g->loopback = loopback;
     g->first = 0;
     g->mem.resize(ndev);
     for (int i = 0; i < ndev; ++i) {
@@ -181,12 +190,14 @@ int mpcqp_group_create(const mpcqp_model *m, int ndev, const int *devices, mpcqp
             return rc;
         }
     }
-    std::vector<ncclComm_t> comms(ndev, nullptr);
-    if (ncclCommInitAll(comms.data(), ndev, devices) != ncclSuccess) {
-        mpcqp_group_destroy(g);
-        return MPCQP_ERR_DEVICE;
+    if (!loopback) {
+        std::vector<ncclComm_t> comms(ndev, nullptr);
+        if (ncclCommInitAll(comms.data(), ndev, devices) != ncclSuccess) {
+            mpcqp_group_destroy(g);
+            return MPCQP_ERR_DEVICE;
+        }
+        for (int i = 0; i < ndev; ++i) g->mem[i].comm = comms[i];
     }
-    for (int i = 0; i < ndev; ++i) g->mem[i].comm = comms[i];
     for (auto &mb : g->mem) {
         const int rc = member_init(g, mb);
         if (rc) {
@@ -274,9 +285,13 @@ int mpcqp_group_solve_select(mpcqp_group *g, const int *B, const int64_t *base,
     for (int i = 0; i < n; ++i) {
         Member &mb = g->mem[i];
         if (hipSetDevice(mb.device) != hipSuccess) return group_fail(g);
-        // rec[p] is free once the all-gather two steps back has read it
-        if (mb.gath_pending[p] && hipStreamWaitEvent(mb.ss, mb.ev_gath[p], 0) != hipSuccess)
-            return group_fail(g);
+        // rec[p] is free once the all-gather two steps back has read it (loopback: every
+        // member's copies read it, each on its own collective stream)
+        for (int j = 0; j < (g->loopback ? n : 1); ++j) {
+            const Member &mj = g->loopback ? g->mem[j] : mb;
+            if (mj.gath_pending[p] && hipStreamWaitEvent(mb.ss, mj.ev_gath[p], 0) != hipSuccess)
+                return group_fail(g);
+        }
         int rc = mpcqp_batch_solve_select(mb.ctx, B[i], x0[i], xref[i], lin[i],
                                           contact ? contact[i] : nullptr, U[i], cost[i],
                                           status[i], iters[i], base[i], mb.rec[p]);
@@ -288,14 +303,30 @@ int mpcqp_group_solve_select(mpcqp_group *g, const int *B, const int64_t *base,
     if (g->step++ == g->inject) return group_fail(g);  // (tests: a failure after the solves)
     // ONE all-gather of the records over all ranks (grouped over this process's members)
     const size_t cnt = 1 + (size_t)g->nV;
-    if (n > 1 && ncclGroupStart() != ncclSuccess) return group_fail(g);
     int rc = MPCQP_OK;
-    for (int i = 0; i < n && !rc; ++i) {
-        Member &mb = g->mem[i];
-        hipSetDevice(mb.device);
-        rc = nccl_rc(ncclAllGather(mb.rec[p], mb.gath[p], cnt, ncclInt64, mb.comm, mb.cs));
+    if (g->loopback) {
+        // (test transport) member i gathers every member's record, after each one is written
+        for (int i = 0; i < n && !rc; ++i) {
+            Member &mb = g->mem[i];
+            hipSetDevice(mb.device);
+            for (int j = 0; j < n && !rc; ++j) {
+                const Member &mj = g->mem[j];
+                rc = hip_rc(hipStreamWaitEvent(mb.cs, mj.ev_rec, 0));
+                if (!rc)
+                    rc = hip_rc(hipMemcpyAsync(mb.gath[p] + (size_t)j * cnt, mj.rec[p],
+                                               sizeof(int64_t) * cnt, hipMemcpyDeviceToDevice,
+                                               mb.cs));
+            }
+        }
+    } else {
+        if (n > 1 && ncclGroupStart() != ncclSuccess) return group_fail(g);
+        for (int i = 0; i < n && !rc; ++i) {
+            Member &mb = g->mem[i];
+            hipSetDevice(mb.device);
+            rc = nccl_rc(ncclAllGather(mb.rec[p], mb.gath[p], cnt, ncclInt64, mb.comm, mb.cs));
+        }
+        if (n > 1 && ncclGroupEnd() != ncclSuccess) rc = MPCQP_ERR_DEVICE;
     }
-    if (n > 1 && ncclGroupEnd() != ncclSuccess) rc = MPCQP_ERR_DEVICE;
     if (rc) return group_fail(g);
     for (int i = 0; i < n; ++i) {
         Member &mb = g->mem[i];

@@ -147,42 +147,36 @@ def test_group_host_path_page_locked_matches(gpu):
     grp.close()
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("gait", ["alternating", "mixed"])
-def test_group_all_devices_matches_whole_batch(gpu, gait):
-    """mpcqp_group_create over every visible device (ncclCommInitAll, the grouped all-gather of
-    the local members, the cross-rank reduction, both record buffers over three steps): each
-    member's best record equals one context's mpcqp_batch_solve_select over the WHOLE batch, bit
-    for bit, and the per-instance outputs of each shard equal that context's.  Needs >= 2
-    devices (src/mpc_control_fake_state.cpp:108-149 at batch scale, SURVEY 8e)."""
+def _group_matches_whole_batch(torch, gait, devices, seed):
+    """a single-process group over `devices` (one rank each): each member's best record equals
+    one context's mpcqp_batch_solve_select over the WHOLE batch, bit for bit, over three steps
+    (both record buffers, one reused), and the per-instance outputs of each shard equal that
+    context's"""
     import mpcqp
     from mpcqp.engine import BatchEngine
     from mpcqp.group import Group, shard
-    torch = gpu
-    ndev = torch.cuda.device_count()
-    if ndev < 2:
-        pytest.skip("one visible device: the multi-device group needs >= 2")
+    nr = len(devices)
     p = mpcqp.model_params("B")
     Cn = 16
-    S = 37 * ndev + 3  # uneven shards
-    batch = mpcqp.make_batch(p, S * Cn, seed=8080, gait=gait)
+    S = 37 * nr + 3  # uneven shards
+    batch = mpcqp.make_batch(p, S * Cn, seed=seed, gait=gait)
     ref = BatchEngine(p, device=0)
     dr = ref.upload(batch)
     rec = torch.zeros(1 + ref.nV, dtype=torch.int64, device="cuda:0")
     ref.solve_select(dr, rec)
     ref.sync()
-    grp = Group(p, devices=list(range(ndev)))
-    assert (grp.local, grp.nranks, grp.first_rank) == (ndev, ndev, 0)
+    grp = Group(p, devices=list(devices))
+    assert (grp.local, grp.nranks, grp.first_rank) == (nr, nr, 0)
     engs, shards = [], []
-    for r in range(ndev):
-        f, n = shard(S, ndev, r)
+    for r in range(nr):
+        f, n = shard(S, nr, r)
         sub = {k: v[f * Cn:(f + n) * Cn] for k, v in batch.items()}
-        e = BatchEngine.wrap(p, grp.ctx(r), r)
+        e = BatchEngine.wrap(p, grp.ctx(r), devices[r])
         d = e.upload(sub)
         engs.append(e)
         shards.append(dict(d, base=f * Cn))
-    steps = [[torch.full((1 + ref.nV,), -5, dtype=torch.int64, device=f"cuda:{r}")
-              for r in range(ndev)] for _ in range(3)]
+    steps = [[torch.full((1 + ref.nV,), -5, dtype=torch.int64, device=f"cuda:{devices[r]}")
+              for r in range(nr)] for _ in range(3)]
     for best in steps:
         grp.solve_select(shards, best)
     grp.sync()
@@ -190,14 +184,44 @@ def test_group_all_devices_matches_whole_batch(gpu, gait):
     for best in steps:
         for b_ in best:
             assert torch.equal(b_.cpu(), want)
-    for r in range(ndev):
-        f, n = shard(S, ndev, r)
+    for r in range(nr):
+        f, n = shard(S, nr, r)
         for k in ("U", "cost", "status", "iters"):
             assert torch.equal(shards[r][k].cpu(), dr[k][f * Cn:(f + n) * Cn].cpu()), (r, k)
+    # the host path over the same group: the whole batch's outputs and record
+    out = grp.solve_select_host(S, Cn, batch)
+    assert np.array_equal(out["best"], want.numpy())
+    for k in ("U", "cost", "status", "iters"):
+        assert np.array_equal(out[k], dr[k].cpu().numpy()), k
     for e in engs:
         e.close()
     grp.close()
     ref.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gait", ["alternating", "mixed"])
+def test_group_all_devices_matches_whole_batch(gpu, gait):
+    """mpcqp_group_create over every visible device (ncclCommInitAll, the grouped all-gather of
+    the local members, the cross-rank reduction): _group_matches_whole_batch.  Needs >= 2
+    devices (src/mpc_control_fake_state.cpp:108-149 at batch scale, SURVEY 8e)."""
+    torch = gpu
+    ndev = torch.cuda.device_count()
+    if ndev < 2:
+        pytest.skip("one visible device: the multi-device group needs >= 2")
+    _group_matches_whole_batch(torch, gait, list(range(ndev)), 8080)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gait", ["alternating", "mixed"])
+def test_group_three_ranks_loopback_matches_whole_batch(gpu, gait, monkeypatch):
+    """three ranks on device 0 over the test transport (MPCQP_GROUP_LOOPBACK=1: the all-gather as
+    device copies, no RCCL): the multi-member orchestration -- uneven shards, per-member solve /
+    collective streams, the record double-buffering across steps, the cross-rank reduction, the
+    host path's per-member staging -- gives every rank the whole batch's record
+    (_group_matches_whole_batch); what it cannot cover is RCCL itself"""
+    monkeypatch.setenv("MPCQP_GROUP_LOOPBACK", "1")
+    _group_matches_whole_batch(gpu, gait, [0, 0, 0], 8181)
 
 
 @pytest.mark.gpu
